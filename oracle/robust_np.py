@@ -1,0 +1,413 @@
+"""CPU oracle: a numpy restatement of the reference's robust aggregators.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path imports this module:
+only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may use it, and there only as the checker / the timed CPU port.  The
+product path (``secure-robust-federated-learning_amd``) fails loudly when its
+HIP library is missing; it never falls back to this file.
+
+Each function restates the algorithm of the reference
+(wanglun1996/secure-robust-federated-learning @ v1, ``src/robust_estimator.py``
+and the inline aggregators of ``src/simulate.py``) from its observable
+behaviour, citing the reference ``file:line`` it follows.  The numpy operations
+are chosen so that the floating-point evaluation order matches the reference
+where that is cheap (sequential axis-0 sums, numpy pairwise sums, BLAS dots),
+which is what makes ``median``/``trimmed_mean``/``bulyan`` bit-exact against the
+golden fixtures in ``tests/golden`` (generated from the live reference by
+``tests/golden/gen_fixtures.py``).
+
+Parity pin: ``tests/test_oracle_golden.py`` checks every function here against
+those fixtures.  The reference ships no golden vectors of its own (SURVEY.md
+§4, §8c), so the fixtures are the only pin.
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.linalg import eigh
+from scipy.special import rel_entr
+
+ITV = 1000        # robust_estimator.py:40
+MAX_ITER = 100    # robust_estimator.py:39 (unused by the reference too)
+
+
+# ----------------------------------------------------------------------------
+# helpers
+# ----------------------------------------------------------------------------
+def _as_rows(samples):
+    """Stack a list of same-shape arrays into (N, D) plus the layer shape."""
+    arr = np.array(samples)
+    return arr.reshape(arr.shape[0], -1), arr.shape[1:]
+
+
+def _l2(v):
+    """np.linalg.norm(v) for ord=None: sqrt(dot(ravel, ravel)) in v's dtype."""
+    flat = v.ravel(order="K")
+    return np.sqrt(flat.dot(flat))
+
+
+def pairwise_l2(rows):
+    """Symmetric matrix of ||x_i - x_j|| (robust_estimator.py:242 evaluates the
+    same BLAS dot per ordered pair; (a-b) and (b-a) give bitwise-equal dots, so
+    only i<j is evaluated here)."""
+    n = len(rows)
+    out = np.zeros((n, n), dtype=np.result_type(rows[0].dtype, np.float32))
+    for i in range(n):
+        for j in range(i + 1, n):
+            out[i, j] = out[j, i] = _l2(rows[i] - rows[j])
+    return out
+
+
+def krum_scores_from_dist(dist, f):
+    """Krum metric from a distance matrix (robust_estimator.py:234-244).
+
+    score_i = numpy pairwise sum of the (n-f-2) smallest distances from i to
+    the other clients, with Python slice semantics for a non-positive count.
+    """
+    n = dist.shape[0]
+    keep = n - f - 2
+    scores = []
+    for i in range(n):
+        others = np.delete(dist[i], i)
+        scores.append(np.sort(others)[:keep].sum())
+    return scores
+
+
+def bucket_count(n, eps, delta):
+    """Bucket count/size of the MoM wrappers (robust_estimator.py:136-137, 211-212),
+    evaluated in float64 exactly as the reference does."""
+    num = int(np.floor(eps * n) + np.log(1.0 / delta))
+    size = int(np.ceil(n * 1.0 / num))
+    return num, size
+
+
+def bucket_means(samples, bucket_size, bucket_num):
+    """Means of consecutive buckets in list order (robust_estimator.py:138-140,
+    213-216, 254-256).  An empty trailing bucket yields a NaN scalar, which the
+    reference's later ``np.array`` rejects with ValueError; reproduce that."""
+    n = len(samples)
+    means = []
+    for b in range(bucket_num):
+        lo, hi = b * bucket_size, min((b + 1) * bucket_size, n)
+        if hi <= lo:
+            raise ValueError("empty bucket %d (N=%d, bucket_size=%d, buckets=%d)"
+                             % (b, n, bucket_size, bucket_num))
+        means.append(np.mean(samples[lo:hi], axis=0))
+    return means
+
+
+def chunk_sizes(feature_size, itv):
+    """itv-wide chunks of a flattened layer, last one partial
+    (robust_estimator.py:116-124, 192-200)."""
+    if itv is None:
+        itv = int(np.floor(np.sqrt(feature_size)))
+    full = int(feature_size // itv)
+    sizes = [itv] * full
+    if feature_size % itv:
+        sizes.append(feature_size - full * itv)
+    return sizes
+
+
+# ----------------------------------------------------------------------------
+# coordinate-wise
+# ----------------------------------------------------------------------------
+def average(samples):
+    """Inline ``--agg average`` (simulate.py:235-244): np.average(axis=0)."""
+    return np.array(samples).mean(axis=0)
+
+
+def median(samples):
+    """robust_estimator.py:220-221: coordinate-wise np.median over clients."""
+    return np.median(np.asarray(samples), axis=0)
+
+
+def trimmed_mean(samples, beta=0.1):
+    """robust_estimator.py:223-232: sort along clients, drop int(N*beta) from
+    each end, mean of the rest (sequential fp32 sum in ascending order)."""
+    stacked = np.array(samples)
+    n = stacked.shape[0]
+    cut = int(n * beta)
+    ordered = np.sort(stacked, axis=0)
+    return ordered[cut:n - cut].mean(axis=0)
+
+
+# ----------------------------------------------------------------------------
+# Krum family
+# ----------------------------------------------------------------------------
+def krum_(samples, f):
+    """robust_estimator.py:234-244 (list of per-client Krum scores)."""
+    rows = [np.asarray(s) for s in samples]
+    return krum_scores_from_dist(pairwise_l2(rows), f)
+
+
+def krum(samples, f):
+    """robust_estimator.py:246-249: the client with the smallest score (first on
+    ties); returns the caller's own object and its index."""
+    scores = krum_(samples, f)
+    idx = int(np.argmin(scores))
+    return samples[idx], idx
+
+
+def mom_krum(samples, f, bucket_size=3):
+    """robust_estimator.py:251-257 (``--agg clustering``, simulate.py:389-397)."""
+    num = int(np.ceil(len(samples) * 1.0 / bucket_size))
+    return krum(bucket_means(samples, bucket_size, num), f=f)[0]
+
+
+# ----------------------------------------------------------------------------
+# Bulyan
+# ----------------------------------------------------------------------------
+def bulyan_median(arr):
+    """robust_estimator.py:259-270 for one coordinate: index minimising the
+    total |a_i - a_j| (numpy pairwise fp64 row sum, first index) and its row."""
+    a = np.asarray(arr, dtype=np.float64)
+    dist = np.abs(a[:, None] - a[None, :])
+    total = dist.sum(axis=-1)
+    m = int(np.argmin(total))
+    return m, dist[m]
+
+
+def bulyan_one_coordinate(arr, beta):
+    """robust_estimator.py:272-275: mean of the beta values nearest the
+    Bulyan median (argsort order, numpy pairwise mean)."""
+    _, row = bulyan_median(arr)
+    return np.mean(np.asarray(arr)[np.argsort(row)[:beta]])
+
+
+def bulyan_coordinates(selected, beta, block=2048):
+    """Vectorised robust_estimator.py:324-330: bulyan_one_coordinate for every
+    coordinate of the (theta, D) float64 matrix ``selected``.
+
+    The (block, theta, theta) distance cube is reduced over its contiguous last
+    axis, which makes numpy use the same pairwise row sum as the reference's
+    per-coordinate theta x theta matrix; argsort/mean run per row with the same
+    kernels as the reference's 1-D calls."""
+    sel = np.ascontiguousarray(np.asarray(selected, dtype=np.float64).T)  # (D, theta)
+    d = sel.shape[0]
+    out = np.empty(d, dtype=np.float64)
+    for lo in range(0, d, block):
+        a = sel[lo:lo + block]
+        cube = np.abs(a[:, :, None] - a[:, None, :])
+        med = cube.sum(axis=-1).argmin(axis=-1)
+        row = cube[np.arange(a.shape[0]), med]
+        order = np.argsort(row, axis=-1)[:, :beta]
+        out[lo:lo + block] = np.take_along_axis(a, order, axis=-1).mean(axis=-1)
+    return out
+
+
+def bulyan_select(rows, f, aggsubfunc):
+    """The theta selection rounds of robust_estimator.py:286-322.
+
+    Returns (selected vectors, trace of removed client indices into ``rows``).
+    ``krum`` appends the Krum-chosen client itself; ``median`` and
+    ``trimmedmean`` append the aggregate vector and then drop the client
+    nearest to it (first strict minimum)."""
+    n = len(rows)
+    theta = n - 2 * f
+    remaining = list(range(n))
+    selected, removed = [], []
+    if aggsubfunc == "krum":
+        dist = pairwise_l2(rows)
+        for _ in range(theta):
+            sub = dist[np.ix_(remaining, remaining)]
+            pick = int(np.argmin(krum_scores_from_dist(sub, f)))
+            client = remaining.pop(pick)
+            selected.append(rows[client])
+            removed.append(client)
+    elif aggsubfunc in ("median", "trimmedmean"):
+        for _ in range(theta):
+            live = [rows[i] for i in remaining]
+            agg = median(live) if aggsubfunc == "median" else trimmed_mean(live)
+            selected.append(agg)
+            best, best_d = None, np.inf
+            for pos, r in enumerate(live):
+                dd = _l2(agg - r)
+                if dd < best_d:
+                    best, best_d = pos, dd
+            assert best is not None
+            removed.append(remaining.pop(best))
+    return selected, removed
+
+
+def bulyan(grads, f, aggsubfunc="trimmedmean"):
+    """robust_estimator.py:277-332."""
+    rows, shape = _as_rows(grads)
+    rows = [r for r in rows]
+    n = len(rows)
+    theta = n - 2 * f
+    if theta <= 0:
+        # the reference indexes an empty selection (robust_estimator.py:327)
+        raise IndexError("bulyan needs N > 2f (theta=%d)" % theta)
+    selected, _ = bulyan_select(rows, f, aggsubfunc)
+    if not selected:
+        raise IndexError("bulyan selected no gradients")
+    sel = np.array([np.asarray(g, dtype=np.float64).ravel() for g in selected])
+    beta = theta - 2 * f
+    return bulyan_coordinates(sel, beta).reshape(shape)
+
+
+# ----------------------------------------------------------------------------
+# spectral filters
+# ----------------------------------------------------------------------------
+def _weighted_cov(centered, c):
+    return (centered.T * c) @ centered / c.sum()
+
+
+def filterL2_(samples, eps=0.2, sigma=1, expansion=20):
+    """robust_estimator.py:144-177 on one (n, k) chunk (primal k x k form)."""
+    x = np.asarray(samples)
+    n0, k = x.shape
+    c = np.ones(n0)
+    for _ in range(2 * int(eps * n0)):
+        mu = np.average(x, axis=0, weights=c)
+        z = x - mu
+        lam, vec = eigh(_weighted_cov(z, c), subset_by_index=[k - 1, k - 1])
+        lam = lam[0]
+        if lam * lam <= expansion * sigma * sigma:
+            return mu
+        tau = (z @ vec[:, 0]) ** 2
+        top = int(np.argmax(tau))
+        c = c * (1 - tau / tau[top])
+        x = np.delete(x, top, axis=0)
+        c = np.delete(c, top)
+        c = c / np.abs(c).sum()
+    return np.average(x, axis=0, weights=c)
+
+
+def _chunked(samples, itv, fn):
+    rows, shape = _as_rows(samples)
+    out, lo = [], 0
+    for size in chunk_sizes(rows.shape[1], itv):
+        out.append(fn(rows[:, lo:lo + size]))
+        lo += size
+    return np.concatenate(out, axis=0).reshape(shape)
+
+
+def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV):
+    """robust_estimator.py:180-208: filterL2_ over itv-wide chunks."""
+    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion))
+
+
+def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
+    """robust_estimator.py:210-218."""
+    num, size = bucket_count(len(samples), eps, delta)
+    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv)
+
+
+def kl_capped_projection(c, eps):
+    """The projection step of robust_estimator.py:77-99: among the candidates
+    that cap the i+1 largest weights at 1/((1-eps)n) and rescale the rest to sum
+    to one, keep the feasible one with the smallest KL(c || c_) (first on ties).
+    Returns None when no candidate is feasible (the reference then fails on the
+    next iteration)."""
+    n = len(c)
+    cap = 1.0 / (1 - eps) / n
+    desc = np.argsort(c)[::-1]
+    best, best_kl = None, None
+    for i in range(n):
+        head, tail = desc[:i + 1], desc[i + 1:]
+        cand = c.copy()
+        cand[head] = cap
+        clip = 1 - cand[head].sum()
+        if clip <= 0:
+            break
+        scale = clip / cand[tail].sum()
+        cand[tail] = cand[tail] * scale
+        if cand[tail[0]] > cap:
+            continue
+        kl = rel_entr(c, cand).sum()
+        if best_kl is None or kl < best_kl:
+            best, best_kl = cand, kl
+    return best
+
+
+def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7):
+    """robust_estimator.py:42-102 on one (n, k) chunk."""
+    x = np.asarray(samples)
+    n = len(x)
+    f = int(np.ceil(eps * n))
+    scores = krum_(list(x), f)
+    keep = np.argpartition(scores, -f)[:-f]
+    x = x[keep]
+    m, k = x.shape
+    far = pairwise_l2(list(x))
+    step = 0.5 / (np.amax(far[np.triu_indices(m, 1)]) ** 2)
+    c = np.ones(m)
+    for _ in range(int(2 * eps * m)):
+        mu = np.average(x, axis=0, weights=c)
+        z = x - mu
+        lam, vec = eigh(_weighted_cov(z, c), subset_by_index=[k - 1, k - 1])
+        lam = lam[0]
+        if lam * lam <= expansion * sigma * sigma:
+            return mu
+        tau = (z @ vec[:, 0]) ** 2
+        c = c * (1 - step * tau)
+        c = kl_capped_projection(c, eps)
+        if c is None:
+            raise TypeError("ex_noregret: no feasible capped-simplex projection")
+    return np.average(x, axis=0, weights=c)
+
+
+def ex_noregret(samples, eps=1. / 12, sigma=1, expansion=20, itv=ITV):
+    """robust_estimator.py:104-133: ex_noregret_ over itv-wide chunks."""
+    return _chunked(samples, itv, lambda ch: ex_noregret_(ch, eps, sigma, expansion))
+
+
+def mom_ex_noregret(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
+    """robust_estimator.py:135-142."""
+    num, size = bucket_count(len(samples), eps, delta)
+    return ex_noregret(bucket_means(samples, size, num), eps, sigma, expansion, itv)
+
+
+# ----------------------------------------------------------------------------
+# stateful inline aggregators of simulate.py
+# ----------------------------------------------------------------------------
+def bucketing_round(layers_by_client, prev, buckets, perround, tau):
+    """simulate.py:335-366 after the (first-round) shuffle of ``choices``:
+    overlapping windows ``choices[b : b + perround//buckets]``, per-bucket mean,
+    cross-layer-norm clipping against ``prev``, then the mean over buckets.
+    ``layers_by_client[c][l]`` is client c's layer l, already in choices order."""
+    width = perround // buckets
+    nlayer = len(prev)
+    bucket_avg = []
+    for b in range(buckets):
+        members = layers_by_client[b:b + width]
+        bucket_avg.append([np.array([m[l] for m in members]).mean(axis=0) for l in range(nlayer)])
+    for b in range(buckets):
+        sq = 0.
+        for l in range(nlayer):
+            sq += _l2(bucket_avg[b][l] - prev[l]) ** 2
+        nrm = np.sqrt(sq)
+        for l in range(nlayer):
+            bucket_avg[b][l] = (bucket_avg[b][l] - prev[l]) * min(1, tau / nrm)
+    return [np.array([bucket_avg[b][l] for b in range(buckets)]).mean(axis=0) for l in range(nlayer)]
+
+
+def history_round(layers_by_client, prev, tau):
+    """simulate.py:367-388: clip every client's update against ``prev`` by the
+    cross-layer norm (in place, as the reference mutates local_grads), then the
+    mean over clients."""
+    nlayer = len(prev)
+    for grads in layers_by_client:
+        sq = 0.
+        for l in range(nlayer):
+            sq += _l2(grads[l] - prev[l]) ** 2
+        nrm = np.sqrt(sq)
+        for l in range(nlayer):
+            grads[l] = (grads[l] - prev[l]) * min(1, tau / nrm)
+    return [np.array([g[l] for g in layers_by_client]).mean(axis=0) for l in range(nlayer)]
+
+
+def as_float32_rows(samples):
+    """Convenience for tests/bench: (N, D) float32 C-contiguous copy."""
+    rows, _ = _as_rows(samples)
+    return np.ascontiguousarray(rows, dtype=np.float32)
+
+
+__all__ = [
+    "ITV", "MAX_ITER", "average", "median", "trimmed_mean", "krum_", "krum",
+    "mom_krum", "bulyan_median", "bulyan_one_coordinate", "bulyan", "filterL2_",
+    "filterL2", "mom_filterL2", "ex_noregret_", "ex_noregret", "mom_ex_noregret",
+    "pairwise_l2", "krum_scores_from_dist", "bucket_count", "bucket_means",
+    "chunk_sizes", "bulyan_coordinates", "bulyan_select", "kl_capped_projection",
+    "bucketing_round", "history_round",
+]

@@ -1,0 +1,69 @@
+"""Shared test configuration.
+
+* registers the ``gpu`` marker (tests that need an MI355X);
+* makes the repo root importable and loads the product package, whose
+  directory name (``secure-robust-federated-learning_amd``) is not a Python
+  identifier, under the import name ``srfl_amd``.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+if GOLDEN not in sys.path:
+    sys.path.insert(0, GOLDEN)
+
+import srfl_loader  # noqa: E402
+
+srfl_loader.load()
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def load_fixture(path):
+    z = np.load(path, allow_pickle=False)
+    rec = {k: z[k] for k in z.files}
+    rec["func"] = str(rec["func"])
+    rec["params"] = json.loads(str(rec["params"]))
+    rec["name"] = os.path.splitext(os.path.basename(path))[0]
+    if "error" in rec:
+        rec["error"] = str(rec["error"])
+    return rec
+
+
+def fixtures(prefix=None, func=None):
+    out = []
+    for p in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
+        if os.path.basename(p).startswith("c1_"):
+            continue
+        rec = load_fixture(p)
+        if prefix and not rec["name"].startswith(prefix):
+            continue
+        if func and rec["func"] != func:
+            continue
+        out.append(rec)
+    return out
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

@@ -1,0 +1,177 @@
+"""Generate the golden fixtures in tests/golden/*.npz from the LIVE reference.
+
+Runs only in the build container, where the reference is mounted read-only at
+/root/reference.  It imports ``src/robust_estimator.py`` with the two shims
+recorded in SURVEY.md §8(c):
+
+  1. ``cvxpy`` is imported at robust_estimator.py:32 but never used and is not
+     installed here -> an empty module is placed in sys.modules;
+  2. scipy 1.15 removed ``eigh(eigvals=...)`` (the reference pins scipy 1.4.1,
+     requirements.txt:3) -> ``robust_estimator.eigh`` is wrapped to map
+     ``eigvals=(lo, hi)`` onto ``subset_by_index=[lo, hi]``.
+
+Only data (inputs, outputs, indices) is written; no reference source or
+bytecode is copied.  Usage:  python tests/golden/gen_fixtures.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+import types
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_SRC = "/root/reference/src"
+sys.path.insert(0, HERE)
+from synth import make_clients, make_convnet_round, CONVNET_MNIST_SHAPES  # noqa: E402
+
+
+def load_reference():
+    if not os.path.isdir(REF_SRC):
+        raise SystemExit("gen_fixtures.py needs the reference at %s; it is never run on the GPU box" % REF_SRC)
+    sys.modules.setdefault("cvxpy", types.ModuleType("cvxpy"))
+    sys.path.insert(0, REF_SRC)
+    import robust_estimator as ref  # noqa: E402
+    from scipy.linalg import eigh as _eigh
+
+    def eigh_compat(a, *args, eigvals=None, **kw):
+        if eigvals is not None:
+            kw["subset_by_index"] = list(eigvals)
+        return _eigh(a, *args, **kw)
+
+    ref.eigh = eigh_compat
+    return ref
+
+
+def save(name, func, params, x, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez(path, func=np.array(func), params=np.array(json.dumps(params)),
+             x=np.asarray(x), **{k: np.asarray(v) for k, v in arrays.items()})
+    print("wrote %-40s %8.1f KB" % (name, os.path.getsize(path) / 1024.0))
+
+
+def run_case(ref, name, func, params, clients, call):
+    t = time.time()
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            res = call()
+    except Exception as e:  # record the reference's failure class
+        save(name, func, params, np.array(clients), error=np.array(type(e).__name__))
+        return
+    extra = {}
+    if isinstance(res, tuple):
+        out, idx = res
+        extra["index"] = np.array(idx)
+        res = out
+    if isinstance(res, list):
+        res = np.array(res)
+    save(name, func, params, np.array(clients), out=res, **extra)
+    _ = t
+
+
+def main():
+    ref = load_reference()
+    cases = []
+
+    # ---- coordinate-wise: median / trimmed_mean / average ----------------
+    cw_shapes = [(1, (7,), 1), (2, (5,), 2), (3, (4, 3), 3), (12, (50,), 4), (100, (30, 30), 5),
+                 (128, (600,), 6), (129, (100,), 7), (512, (64,), 8), (128, (1,), 9), (16, (33,), 10)]
+    for n, shp, seed in cw_shapes:
+        xs = make_clients(n, shp, seed)
+        cases.append(("median_n%d_%s" % (n, "x".join(map(str, shp))), "median", {}, xs,
+                      (lambda xs=xs: ref.median(xs))))
+        cases.append(("trimmed_mean_n%d_%s" % (n, "x".join(map(str, shp))), "trimmed_mean", {"beta": 0.1}, xs,
+                      (lambda xs=xs: ref.trimmed_mean(xs))))
+    for beta in (0.0, 0.2, 0.45):
+        xs = make_clients(40, (77,), 11)
+        cases.append(("trimmed_mean_beta%g" % beta, "trimmed_mean", {"beta": beta}, xs,
+                      (lambda xs=xs, beta=beta: ref.trimmed_mean(xs, beta))))
+    # NaN / inf / ties
+    xs = make_clients(20, (40,), 12)
+    xs[3][5] = np.nan
+    xs[7][9] = np.nan
+    xs[8][9] = np.nan
+    xs[1][10] = np.nan
+    xs[2][10] = np.nan
+    xs[4][10] = np.nan   # 3 NaNs at coord 10 > b=2 -> NaN; 2 at coord 9 trimmed
+    xs[5][11] = np.inf
+    xs[6][12] = -np.inf
+    xs[9][13] = np.inf
+    xs[10][13] = -np.inf
+    cases.append(("median_nan_inf", "median", {}, xs, (lambda xs=xs: ref.median(xs))))
+    cases.append(("trimmed_mean_nan_inf", "trimmed_mean", {"beta": 0.1}, xs, (lambda xs=xs: ref.trimmed_mean(xs))))
+    rng = np.random.default_rng(13)
+    ties = [rng.integers(-3, 4, size=(25,)).astype(np.float32) for _ in range(31)]
+    cases.append(("median_ties", "median", {}, ties, (lambda xs=ties: ref.median(xs))))
+    cases.append(("trimmed_mean_ties", "trimmed_mean", {"beta": 0.1}, ties, (lambda xs=ties: ref.trimmed_mean(xs))))
+
+    # ---- Krum / MoM-Krum ---------------------------------------------------
+    for n, f, shp, seed, kw in [(5, 1, (6,), 20, {}), (12, 2, (3, 7), 21, {}), (30, 5, (64,), 22, {"byz": 5}),
+                                (10, 9, (8,), 23, {}), (10, 8, (8,), 24, {}),
+                                (64, 10, (200,), 25, {"byz": 10, "identical_byz": True}),
+                                (128, 20, (300,), 26, {"byz": 20})]:
+        xs = make_clients(n, shp, seed, **kw)
+        cases.append(("krum_n%d_f%d" % (n, f), "krum", {"f": f}, xs, (lambda xs=xs, f=f: ref.krum(xs, f))))
+        cases.append(("krum__n%d_f%d" % (n, f), "krum_", {"f": f}, xs, (lambda xs=xs, f=f: ref.krum_(xs, f))))
+    for n, f, seed in [(30, 3, 30), (100, 20, 31), (128, 20, 32)]:
+        xs = make_clients(n, (120,), seed, byz=f)
+        cases.append(("mom_krum_n%d_f%d" % (n, f), "mom_krum", {"f": f}, xs, (lambda xs=xs, f=f: ref.mom_krum(xs, f))))
+
+    # ---- Bulyan --------------------------------------------------------------
+    for n, f, shp, seed, kw in [(24, 5, (40,), 40, {}), (30, 5, (12, 10), 41, {"byz": 5}),
+                                (45, 10, (90,), 42, {"byz": 10}), (40, 9, (70,), 43, {"byz": 9, "identical_byz": True}),
+                                (100, 20, (300,), 44, {"byz": 20})]:
+        xs = make_clients(n, shp, seed, **kw)
+        for mode in ("krum", "median", "trimmedmean"):
+            cases.append(("bulyan_%s_n%d_f%d" % (mode, n, f), "bulyan", {"f": f, "aggsubfunc": mode}, xs,
+                          (lambda xs=xs, f=f, mode=mode: ref.bulyan(xs, f, aggsubfunc=mode))))
+    xs = make_clients(10, (5,), 45)
+    cases.append(("bulyan_theta0", "bulyan", {"f": 5, "aggsubfunc": "trimmedmean"}, xs,
+                  (lambda xs=xs: ref.bulyan(xs, 5, aggsubfunc="trimmedmean"))))
+
+    # ---- spectral filters ----------------------------------------------------
+    for tag, n, shp, seed, kw, params in [
+        ("exit", 30, (40,), 50, {"byz": 5}, {"eps": 0.2, "sigma": 0.02, "expansion": 20, "itv": 20}),
+        ("noexit", 30, (40,), 51, {"byz": 5}, {"eps": 0.2, "sigma": 1e-5, "expansion": 20, "itv": 20}),
+        ("sqrt_itv", 40, (7, 9), 52, {"byz": 8}, {"eps": 0.2, "sigma": 0.02, "expansion": 20, "itv": None}),
+        ("ragged", 24, (53,), 53, {"byz": 4}, {"eps": 0.2, "sigma": 0.02, "expansion": 20, "itv": 16}),
+    ]:
+        xs = make_clients(n, shp, seed, **kw)
+        cases.append(("filterL2_%s" % tag, "filterL2", params, xs,
+                      (lambda xs=xs, p=params: ref.filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+        cases.append(("ex_noregret_%s" % tag, "ex_noregret", params, xs,
+                      (lambda xs=xs, p=params: ref.ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+    for tag, n, seed, params in [
+        ("ok", 40, 60, {"eps": 0.2, "sigma": 0.02, "expansion": 20, "itv": 25, "delta": float(np.exp(-2))}),
+        ("empty_bucket", 128, 61, {"eps": 0.2, "sigma": 1e-5, "expansion": 20, "itv": 25, "delta": float(np.exp(-30))}),
+    ]:
+        xs = make_clients(n, (50,), seed, byz=int(0.2 * n))
+        cases.append(("mom_filterL2_%s" % tag, "mom_filterL2", params, xs,
+                      (lambda xs=xs, p=params: ref.mom_filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"], p["delta"]))))
+        cases.append(("mom_ex_noregret_%s" % tag, "mom_ex_noregret", params, xs,
+                      (lambda xs=xs, p=params: ref.mom_ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"], p["delta"]))))
+
+    for name, func, params, xs, call in cases:
+        run_case(ref, name, func, params, xs, call)
+
+    # ---- C1 plumbing: one round of the ConvNet layers at N=100 ------------
+    seed = 70
+    layers = make_convnet_round(100, seed)
+    outs = {}
+    for agg, fn in (("median", ref.median), ("trimmedmean", ref.trimmed_mean)):
+        outs[agg] = np.concatenate([fn(lay).ravel() for lay in layers]).astype(np.float32)
+    kr = [ref.krum(lay, 20)[1] for lay in layers]
+    np.savez(os.path.join(HERE, "c1_convnet_n100.npz"), seed=np.array(seed), n=np.array(100),
+             shapes=np.array(json.dumps(CONVNET_MNIST_SHAPES)), median=outs["median"],
+             trimmedmean=outs["trimmedmean"], krum_index=np.array(kr),
+             x_checksum=np.array([float(np.sum(np.stack(l).astype(np.float64))) for l in layers]))
+    print("wrote c1_convnet_n100")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,75 @@
+"""Pin the CPU oracle (oracle/robust_np.py) against the golden fixtures that
+tests/golden/gen_fixtures.py generated from the live reference.
+
+Bit-exact where the restatement follows the reference's evaluation order
+(average, median, trimmed_mean, krum scores/index, bulyan); the spectral
+filters evaluate the weighted covariance with one GEMM instead of the
+reference's stacked outer products, so they are pinned at fp64 rounding level.
+"""
+from __future__ import annotations
+
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import fixtures, GOLDEN
+from oracle import robust_np as orc
+from synth import make_convnet_round
+
+CALL = {
+    "median": lambda xs, p: orc.median(xs),
+    "trimmed_mean": lambda xs, p: orc.trimmed_mean(xs, p.get("beta", 0.1)),
+    "krum": lambda xs, p: orc.krum(xs, p["f"]),
+    "krum_": lambda xs, p: orc.krum_(xs, p["f"]),
+    "mom_krum": lambda xs, p: orc.mom_krum(xs, p["f"]),
+    "bulyan": lambda xs, p: orc.bulyan(xs, p["f"], p["aggsubfunc"]),
+    "filterL2": lambda xs, p: orc.filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]),
+    "ex_noregret": lambda xs, p: orc.ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]),
+    "mom_filterL2": lambda xs, p: orc.mom_filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"], p["delta"]),
+    "mom_ex_noregret": lambda xs, p: orc.mom_ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"], p["delta"]),
+}
+EXACT = {"median", "trimmed_mean", "krum", "krum_", "mom_krum", "bulyan"}
+
+CASES = fixtures()
+
+
+@pytest.mark.parametrize("rec", CASES, ids=[r["name"] for r in CASES])
+def test_oracle_matches_reference(rec):
+    xs = [rec["x"][i] for i in range(rec["x"].shape[0])]
+    call = CALL[rec["func"]]
+    if "error" in rec:
+        exc = {"IndexError": IndexError, "ValueError": ValueError, "TypeError": TypeError}[rec["error"]]
+        with pytest.raises(exc), warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            call(xs, rec["params"])
+        return
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        got = call(xs, rec["params"])
+    if isinstance(got, tuple):
+        got, idx = got
+        assert idx == int(rec["index"])
+    got = np.asarray(got)
+    want = rec["out"]
+    assert got.shape == want.shape
+    if rec["func"] in EXACT:
+        np.testing.assert_array_equal(got, want)
+        if rec["func"] != "krum_":
+            assert got.dtype == want.dtype
+    else:
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
+
+
+def test_oracle_c1_convnet_round():
+    z = np.load(os.path.join(GOLDEN, "c1_convnet_n100.npz"))
+    layers = make_convnet_round(int(z["n"]), int(z["seed"]))
+    cs = [float(np.sum(np.stack(l).astype(np.float64))) for l in layers]
+    np.testing.assert_array_equal(np.array(cs), z["x_checksum"])
+    med = np.concatenate([orc.median(l).ravel() for l in layers])
+    tm = np.concatenate([orc.trimmed_mean(l).ravel() for l in layers])
+    np.testing.assert_array_equal(med, z["median"])
+    np.testing.assert_array_equal(tm, z["trimmedmean"])
+    assert json.loads(str(z["shapes"]))[4] == [200, 1470]
