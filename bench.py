@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: aggregated-gradient GB/s (device-resident N x d fp32) on MI355X.
+
+Default workload (BASELINE.json north star): coordinate-wise trimmed mean over
+N=128 clients x d=1e8 fp32 per GPU, i.e. 51.2 GB of client updates resident
+in HBM per GPU.  One "step" = one aggregation call over the whole N x d
+matrix.  With --gpus > 1 (torch.distributed.run, one rank per GPU) the
+gradient dimension is sharded: every rank aggregates its own d-shard (fixed
+per-GPU work -> weak scaling) and the aggregate is assembled on every rank by
+one RCCL all-gather over xGMI, which is part of the timed step.
+
+value = N * d_total * 4 bytes / (max over ranks of the timed region) in GB/s.
+
+Extra fields on the JSON line:
+  roofline     — dominant kernel (the k-select) timed with HIP events on the
+                 launch stream; achieved = algorithmic bytes per launch
+                 (4*N*d + 4*d) / average launch duration; peak = 8000 GB/s.
+  cpu_baseline — the numpy restatement of robust_estimator.trimmed_mean
+                 (oracle/robust_np.py, kind "port") timed on this host on a
+                 bounded sample (rank 0, N=1 only).
+  host_inclusive — H2D + kernel + D2H rate from pinned host memory (the
+                 simulator hands host arrays over); never `value`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import srfl_loader  # noqa: E402
+
+srfl = srfl_loader.load()
+from srfl_amd import engine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--agg", default="trimmedmean", choices=["trimmedmean", "median", "average"])
+    ap.add_argument("--clients", type=int, default=128)
+    ap.add_argument("--d", type=float, default=1e8, help="coordinates per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes from rocprofv3 PMC (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+AGG = {
+    "trimmedmean": lambda X, out: engine.trimmed_mean(X, 0.1, out=out),
+    "median": lambda X, out: engine.median(X, out=out),
+    "average": lambda X, out: engine.average(X, out=out),
+}
+KERNEL_NAME = {
+    "trimmedmean": "select_reg_kernel<128, 1>",
+    "median": "select_reg_kernel<128, 0>",
+    "average": "average_vec4_kernel",
+}
+
+
+def cpu_baseline(agg, n, budget_s):
+    """Time the oracle's CPU port on N x 1e6 chunks until ~budget_s elapsed."""
+    from oracle import robust_np as orc
+    fn = {"trimmedmean": orc.trimmed_mean, "median": orc.median, "average": orc.average}[agg]
+    d = 1_000_000
+    rng = np.random.default_rng(0)
+    x = (0.01 * rng.standard_normal((n, d))).astype(np.float32)
+    samples = list(x)
+    fn(samples)  # warm
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        fn(samples)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or reps >= 200:
+            break
+    gbs = reps * n * d * 4 / el / 1e9
+    return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "%d x numpy %s over N=%d x d=1e6 fp32 (oracle/robust_np.py), %.1f s on host cores, single thread"
+                      % (reps, agg, n, el)}
+
+
+def host_inclusive(agg, n, device):
+    """Pinned host N x d -> device, aggregate, result -> host (d = 4e6)."""
+    d = 4_000_000
+    host = torch.empty((n, d), dtype=torch.float32, pin_memory=True)
+    host.normal_(0, 0.01)
+    res = torch.empty(d, dtype=torch.float32, pin_memory=True)
+    X = torch.empty((n, d), dtype=torch.float32, device=device)
+    out = torch.empty(d, dtype=torch.float32, device=device)
+    for _ in range(2):
+        X.copy_(host, non_blocking=True); AGG[agg](X, out); res.copy_(out, non_blocking=True)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        X.copy_(host, non_blocking=True)
+        AGG[agg](X, out)
+        res.copy_(out, non_blocking=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(reps * n * d * 4 / el / 1e9, 2), "unit": "GB/s", "d": d,
+            "note": "pinned H2D + kernel + D2H per call, serial on one stream"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    n = a.clients
+    d = int(a.d)
+    # synthetic client updates, resident in HBM (fixed seed per rank)
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    X = torch.empty((n, d), dtype=torch.float32, device=device)
+    rows_per = max(1, int(2e9 // (4 * d)) or 1)
+    for r0 in range(0, n, rows_per):
+        X[r0:r0 + rows_per].normal_(0.0, 0.01, generator=g)
+    out = torch.empty(d, dtype=torch.float32, device=device)
+    full = torch.empty(d * world, dtype=torch.float32, device=device) if world > 1 else None
+    fn = AGG[a.agg]
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        fn(X, out)
+        if ev is not None:
+            ev[1].record()
+        if world > 1:
+            dist.all_gather_into_tensor(full, out)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(s.elapsed_time(e) for s, e in evs) / a.steps
+    ms_per_step = elapsed * 1e3 / a.steps
+    total_bytes = n * d * world * 4
+    value = total_bytes / (elapsed / a.steps) / 1e9
+
+    alg_bytes = 4 * n * d + 4 * d
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(a.traffic_json) as fh:
+            tj = json.load(fh)
+        rec = tj.get("%s:N=%d:d=%d" % (a.agg, n, d))
+        if rec:
+            traffic = rec["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        traffic = None
+    line = {
+        "metric": "aggregated-gradient GB/s (device-resident, N x d fp32)",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: N(0, 0.01) fp32 client updates generated on device",
+        "config": {"workload": "%s N=%d clients x d=%.0e fp32 per GPU%s" % (
+                       a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
+                   "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
+                   "parallelism": "d-shard x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": KERNEL_NAME[a.agg], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1 and not a.no_host:
+        del X
+        torch.cuda.empty_cache()
+        line["host_inclusive"] = host_inclusive(a.agg, n, device)
+    if rank == 0 and world == 1 and not a.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(a.agg, n, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+/*
+ * sra.h — C ABI of the MI355X-native Byzantine-robust gradient-reduction
+ * engine ("SRA": secure robust aggregation), libsra.so.
+ *
+ * Each entry point replaces one aggregator of the reference
+ * (wanglun1996/secure-robust-federated-learning @ v1); the reference symbol it
+ * replaces is cited per function.  The reference is pure Python, so the
+ * "binding a maintainer would add" is the ctypes layer in
+ * secure-robust-federated-learning_amd/_lib.py.
+ *
+ * Conventions (all entry points):
+ *  - X is a device pointer to an N x d float32 matrix, client-major: client i's
+ *    flattened update is X[i*ldx .. i*ldx+d).  ldx >= d (elements).
+ *  - All pointers are device pointers owned by the caller; nothing is
+ *    allocated on the hot path (workspace comes from the *_workspace query).
+ *  - Calls are asynchronous and ordered on `stream` (a hipStream_t; NULL = the
+ *    legacy default stream).
+ *  - Return 0 (SRA_OK) or a negative sra_status; sra_last_error() gives a
+ *    thread-local message.  No global mutable state.
+ */
+#ifndef SRA_H_
+#define SRA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  SRA_OK = 0,
+  SRA_ERR_ARG = -1,          /* bad pointer / size / parameter       -> ValueError   */
+  SRA_ERR_SHAPE = -2,        /* inconsistent N, d, ldx              -> ValueError   */
+  SRA_ERR_UNSUPPORTED = -3,  /* N or mode outside what is built     -> NotImplementedError */
+  SRA_ERR_EMPTY_BUCKET = -4, /* MoM bucket with no member           -> ValueError   */
+  SRA_ERR_THETA = -5,        /* Bulyan theta <= 0                    -> IndexError   */
+  SRA_ERR_HIP = -6,          /* HIP runtime error                    -> RuntimeError */
+  SRA_ERR_WORKSPACE = -7,    /* workspace too small                  -> ValueError   */
+  SRA_ERR_INFEASIBLE = -8    /* no feasible capped-simplex projection-> TypeError    */
+} sra_status;
+
+/* Thread-local text of the last error on this thread. */
+const char* sra_last_error(void);
+
+/* ABI version (major*10000 + minor*100 + patch). */
+int sra_version(void);
+
+/* Largest client count served by the register-resident k-select path
+ * (larger N goes through the LDS path). */
+int sra_max_register_clients(void);
+
+/* ------------------------------------------------------------------------ */
+/* Coordinate-wise aggregators (k1: per-coordinate k-select)                 */
+/* ------------------------------------------------------------------------ */
+
+/* out[j] = mean_i X[i, j]: sequential fp32 sum over clients in order, then /N.
+ * Replaces the inline `--agg average` of src/simulate.py:235-244
+ * (np.average(axis=0)). */
+int sra_average_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* out, void* stream);
+
+/* Coordinate-wise median, numpy semantics: even N -> (s[N/2-1]+s[N/2])/2 in
+ * fp32, odd N -> s[(N-1)/2]; any NaN in a column -> NaN.
+ * Replaces robust_estimator.median (src/robust_estimator.py:220-221). */
+int sra_median_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* out, void* stream);
+
+/* Coordinate-wise trimmed mean: sort each column (NaN last), drop b values at
+ * each end, sum the rest sequentially in ascending order in fp32, divide by
+ * N-2b.  Bit-exact with robust_estimator.trimmed_mean
+ * (src/robust_estimator.py:223-232) for d > 1; b = int(N*beta) is computed by
+ * the caller exactly as the reference does. */
+int sra_trimmed_mean_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t b, float* out,
+                         void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRA_H_ */

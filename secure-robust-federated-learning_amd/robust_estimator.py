@@ -1,0 +1,107 @@
+"""Drop-in replacement of the reference module ``robust_estimator``
+(src/robust_estimator.py), computed on the MI355X by libsra.
+
+Same names, signatures, defaults and return types as the reference (SURVEY.md
+§8(b)).  ``samples`` may be
+
+* a list of same-shape numpy arrays (the reference's calling convention,
+  simulate.py:277-279): results come back as numpy arrays of the layer shape
+  in the dtype numpy would return;
+* a list of torch tensors, or one (N, *shape) torch tensor, on the GPU: the
+  result stays on the GPU as a torch tensor (no host round trip).
+
+Arithmetic is fp32 on the device.  Inputs numpy promotes to float64 (an
+attack's float64 rows, reference src/attack.py:197,260) are computed in fp32
+and returned as float64 (tolerance stated in DESIGN.md).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import engine
+
+ITV = 1000        # reference robust_estimator.py:40
+MAX_ITER = 100    # reference robust_estimator.py:39
+
+
+class _Staged:
+    """An (N, D) float32 device matrix plus what is needed to hand results back."""
+
+    def __init__(self, X, shape, np_dtype, device_io, n):
+        self.X = X
+        self.shape = shape
+        self.np_dtype = np_dtype
+        self.device_io = device_io
+        self.n = n
+
+    def result(self, vec, dtype=None):
+        """Return a flat device vector in the caller's convention."""
+        if self.device_io:
+            return vec.reshape(self.shape)
+        out = vec.detach().to("cpu").numpy().reshape(self.shape)
+        want = dtype if dtype is not None else self.np_dtype
+        return out.astype(want, copy=False)
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("srfl_amd.robust_estimator needs an MI355X (HIP device); no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stage(samples):
+    """Stack the caller's samples into one (N, D) float32 device matrix."""
+    if isinstance(samples, torch.Tensor):
+        if samples.dim() < 1:
+            raise ValueError("samples must have a leading client axis")
+        n = samples.shape[0]
+        shape = tuple(samples.shape[1:])
+        X = samples.reshape(n, -1)
+        device_io = samples.is_cuda
+        if not device_io:
+            X = X.to(_device())
+        return _Staged(X.to(torch.float32).contiguous(), shape, _np_dtype(samples.dtype), device_io, n)
+    seq = list(samples)
+    if not seq:
+        raise ValueError("need at least one sample")
+    if isinstance(seq[0], torch.Tensor):
+        shape = tuple(seq[0].shape)
+        X = torch.stack([t.reshape(-1) for t in seq])
+        device_io = X.is_cuda
+        if not device_io:
+            X = X.to(_device())
+        return _Staged(X.to(torch.float32).contiguous(), shape, _np_dtype(seq[0].dtype), device_io, len(seq))
+    arr = np.array(seq)                       # the reference's own stacking (robust_estimator.py:224)
+    n = arr.shape[0]
+    shape = arr.shape[1:]
+    res_dtype = np.result_type(arr.dtype, np.float32) if arr.dtype.kind != "f" else arr.dtype
+    host = torch.empty((n, int(np.prod(shape, dtype=np.int64))), dtype=torch.float32, pin_memory=True)
+    host.numpy()[...] = arr.reshape(n, -1)
+    X = host.to(_device(), non_blocking=True)
+    return _Staged(X, shape, res_dtype, False, n)
+
+
+def _np_dtype(tdtype):
+    return {torch.float64: np.float64, torch.float16: np.float16}.get(tdtype, np.float32)
+
+
+# ---------------------------------------------------------------------------
+# coordinate-wise
+# ---------------------------------------------------------------------------
+def median(samples):
+    """robust_estimator.py:220-221 (np.median(samples, axis=0))."""
+    st = _stage(samples)
+    return st.result(engine.median(st.X))
+
+
+def trimmed_mean(samples, beta=0.1):
+    """robust_estimator.py:223-232."""
+    st = _stage(samples)
+    return st.result(engine.trimmed_mean(st.X, beta))
+
+
+def average(samples):
+    """The inline ``--agg average`` of simulate.py:235-244 (np.average(axis=0))."""
+    st = _stage(samples)
+    return st.result(engine.average(st.X))

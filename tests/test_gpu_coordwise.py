@@ -1,0 +1,92 @@
+"""GPU parity of the coordinate-wise aggregators (k1) against the oracle and the
+golden fixtures: bit-exact (assert_array_equal) for average, median and
+trimmed_mean at every size, including the ragged / NaN / inf / tie cases."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import fixtures, gpu_available, GOLDEN
+from oracle import robust_np as orc
+from synth import make_rows, make_convnet_round
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from srfl_amd import engine, robust_estimator as gre
+
+CW = fixtures(func="median") + fixtures(func="trimmed_mean")
+
+
+@pytest.mark.parametrize("rec", CW, ids=[r["name"] for r in CW])
+def test_golden_coordwise(rec):
+    xs = [rec["x"][i] for i in range(rec["x"].shape[0])]
+    if rec["func"] == "median":
+        got = gre.median(xs)
+    else:
+        got = gre.trimmed_mean(xs, rec["params"]["beta"])
+    want = rec["out"]
+    assert got.shape == want.shape and got.dtype == want.dtype
+    if want.size == 1 and rec["func"] == "trimmed_mean" and rec["x"].shape[0] > 8:
+        # numel == 1: numpy switches to a pairwise sum; fp32 tolerance
+        np.testing.assert_allclose(got, want, rtol=2e-6, atol=1e-9)
+    else:
+        np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 15, 16, 17, 31, 33, 64, 65, 99, 100, 101, 127, 128, 129, 200, 256, 512, 1000])
+def test_every_register_and_lds_bucket(n):
+    d = 1031  # not a multiple of 4 / 256: exercises tail lanes
+    x = make_rows(n, d, seed=1000 + n)
+    X = torch.from_numpy(x).cuda()
+    np.testing.assert_array_equal(engine.median(X).cpu().numpy(), orc.median(list(x)))
+    np.testing.assert_array_equal(engine.trimmed_mean(X, 0.1).cpu().numpy(), orc.trimmed_mean(list(x)))
+    np.testing.assert_array_equal(engine.average(X).cpu().numpy(), orc.average(list(x)))
+
+
+@pytest.mark.parametrize("beta", [0.0, 0.05, 0.25, 0.49, 0.5, 0.7])
+def test_trim_fractions(beta):
+    x = make_rows(100, 777, seed=7)
+    got = engine.trimmed_mean(torch.from_numpy(x).cuda(), beta).cpu().numpy()
+    with np.errstate(all="ignore"):
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            want = orc.trimmed_mean(list(x), beta)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_strided_rows_and_vec4_average():
+    x = make_rows(64, 4096, seed=3)
+    big = torch.from_numpy(x).cuda()
+    sub = big[:, 5:5 + 3000]                      # ldx = 4096 != d, unaligned base
+    np.testing.assert_array_equal(engine.trimmed_mean(sub).cpu().numpy(), orc.trimmed_mean(list(x[:, 5:3005])))
+    np.testing.assert_array_equal(engine.average(big).cpu().numpy(), orc.average(list(x)))   # vec4 path
+    np.testing.assert_array_equal(engine.average(sub).cpu().numpy(), orc.average(list(x[:, 5:3005])))
+
+
+def test_c1_convnet_round_bitexact():
+    z = np.load(GOLDEN + "/c1_convnet_n100.npz")
+    layers = make_convnet_round(int(z["n"]), int(z["seed"]))
+    med = np.concatenate([gre.median(l).ravel() for l in layers])
+    tm = np.concatenate([gre.trimmed_mean(l).ravel() for l in layers])
+    np.testing.assert_array_equal(med, z["median"])
+    np.testing.assert_array_equal(tm, z["trimmedmean"])
+
+
+def test_full_size_properties():
+    """C2 size (N=128, d=1e6): permutation invariance (bitwise) and the exact
+    oracle on a 1e5-coordinate slice; device tensors in, device tensors out."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = 0.01 * torch.randn(128, 1_000_000, device="cuda", generator=g)
+    tm = engine.trimmed_mean(X)
+    perm = torch.randperm(128, device="cuda", generator=g)
+    assert torch.equal(tm, engine.trimmed_mean(X[perm].contiguous()))
+    md = engine.median(X)
+    assert torch.equal(md, engine.median(X[perm].contiguous()))
+    sl = X[:, :100_000].cpu().numpy()
+    np.testing.assert_array_equal(tm[:100_000].cpu().numpy(), orc.trimmed_mean(list(sl)))
+    np.testing.assert_array_equal(md[:100_000].cpu().numpy(), orc.median(list(sl)))
+    out = gre.trimmed_mean(X)            # device in -> device out
+    assert out.is_cuda and torch.equal(out, tm)
