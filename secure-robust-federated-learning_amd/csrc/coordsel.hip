@@ -23,6 +23,8 @@
 // N > 128 (e.g. the N=512 MoM/8-GPU config) uses an LDS bitonic path.
 #include "sra_common.hpp"
 
+#include <cstdlib>
+
 namespace sra {
 
 enum SelectMode { kMedian = 0, kTrimmed = 1 };
@@ -95,56 +97,205 @@ __device__ __forceinline__ float ldrow(const char* row, unsigned off) {
   return __builtin_nontemporal_load(reinterpret_cast<gfloat*>(u));
 }
 
-template <int P, int MODE>
-__global__ void __launch_bounds__(256) select_reg_kernel(const float* __restrict__ X, int n, int64_t d,
-                                                        int64_t ldx, int lo, int hi, float* __restrict__ out) {
+template <int P, int MODE, int NX = 0, int BX = -1, int BS = 256>
+__global__ void __launch_bounds__(BS) select_reg_kernel(const float* __restrict__ X, int n_rt, int64_t d,
+                                                       int64_t ldx, int lo_rt, int hi_rt, float* __restrict__ out) {
   constexpr int P2 = next_pow2(P);
-  constexpr int kFirstPad = (P > 16) ? P - 16 : 0;  // rows below this are always real
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x;
+  constexpr bool kExactN = NX > 0;
+  constexpr bool kExactB = kExactN && BX >= 0;
+  const int n = kExactN ? NX : n_rt;
+  const int lo = kExactB ? BX : lo_rt;
+  const int hi = kExactB ? NX - BX : hi_rt;
+  constexpr int kFirstPad = kExactN ? NX : ((P > 16) ? P - 16 : 0);  // rows below this are always real
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * BS;
   const int64_t rem = d - base;                    // > 0
   const unsigned t = threadIdx.x;
-  const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
+  const unsigned last = rem < BS ? static_cast<unsigned>(rem - 1) : static_cast<unsigned>(BS - 1);
   const unsigned off = (t < last ? t : last) * 4u;  // byte offset of this lane (tail lanes clamped)
   const char* xb = reinterpret_cast<const char*>(X + base);
   const int64_t ldb = ldx * 4;
-  const int k_bottom = (MODE == kMedian) ? (P - n) / 2 : 0;  // -inf pads for the median
+  // exact-N instantiations have no runtime pads: slots [NX, P2) are implicit
+  // +inf and the requested order statistics sit on fixed slots
+  constexpr int PR = kExactN ? NX : P;
+  const int k_bottom = (MODE == kMedian && !kExactN) ? (P - n) / 2 : 0;  // -inf pads (runtime-N median)
   float v[P2];
 #pragma unroll
-  for (int i = 0; i < kFirstPad; ++i) v[i] = ldrow(xb + i * ldb, off);
+  for (int i = 0; i < kFirstPad; ++i) {
+    v[i] = ldrow(xb + i * ldb, off);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
-  for (int i = kFirstPad; i < P; ++i) {
+  for (int i = kFirstPad; i < PR; ++i) {
     const int r = i < n ? i : n - 1;
     const float x = ldrow(xb + r * ldb, off);
-    const float pad = (i - n < k_bottom) ? -__builtin_inff() : qnan();
+    __builtin_amdgcn_sched_barrier(0);
+    const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
     v[i] = i < n ? x : pad;
   }
 
+  // Median slots: runtime N centres the real values between the -inf/+inf
+  // pads (slots P/2-1, P/2); exact N keeps them at the front.
+  constexpr int kMedLo = kExactN ? (NX - 1) / 2 : P / 2 - 1;
+  constexpr int kMedHi = kExactN ? NX / 2 : P / 2;
+  constexpr int kOutLo = MODE == kMedian ? kMedLo : (kExactB ? BX : 0);
+  constexpr int kOutHi = MODE == kMedian ? kMedHi + 1 : (kExactB ? NX - BX : PR);
+
+  // NaNs (rare, wave-uniform branch): a NaN-propagating max over the raw
+  // values detects them; they are then counted and mapped to +inf, which sorts
+  // them last exactly like numpy; the count decides afterwards whether a NaN
+  // lands in the kept range.  The network itself is NaN-free.
+  float m = v[0];
+#pragma unroll
+  for (int i = 1; i < PR; ++i) m = __builtin_elementwise_maximum(m, v[i]);
+  int nan_cnt = 0;
+  if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
+#pragma unroll
+    for (int i = 0; i < PR; ++i) {
+      const bool isn = __builtin_isnan(v[i]);
+      nan_cnt += isn ? 1 : 0;
+      v[i] = isn ? __builtin_inff() : v[i];
+    }
+  }
+  network_fast<P2, PR, kOutLo, kOutHi>(v);
+
   float res;
   if constexpr (MODE == kMedian) {
-    float m = v[0];
-#pragma unroll
-    for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, v[i]);  // NaN-propagating
-    sort_network<P2, P, P / 2 - 1, P / 2 + 1>(v);
-    res = (n & 1) ? v[P / 2 - 1] : (v[P / 2 - 1] + v[P / 2]) * 0.5f;
-    if (__builtin_isnan(m)) res = qnan();
+    const float a = kExactN ? v[kMedLo] : v[P / 2 - 1];
+    const float b = kExactN ? v[kMedHi] : v[P / 2];
+    res = (n & 1) ? a : (a + b) * 0.5f;
+    if (nan_cnt > 0) res = qnan();
   } else {
-    sort_network<P2, P, 0, P>(v);
     // sequential ascending-order sum of s[lo .. hi), numpy's axis-0 reduce;
-    // out-of-range positions contribute +0 (acc + 0 == acc), so the order of
-    // the kept terms is exactly numpy's
-    // (the empty volatile asm keeps each predicate a wave-uniform scalar
-    // branch instead of 128 hoisted SGPR-pair masks that spill)
+    // (the empty volatile asm keeps each runtime predicate a wave-uniform
+    // scalar branch instead of hoisted SGPR-pair masks that spill)
     float acc = 0.f;
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
+    for (int p = 0; p < PR; ++p) {
       if (p >= lo && p < hi) {
-        asm volatile("");
+        if constexpr (!kExactB) asm volatile("");
         acc += v[p];
       }
     }
     res = acc / static_cast<float>(hi - lo);
+    if (nan_cnt > n - hi) res = qnan();   // a NaN sits in the kept range
   }
   if (t < rem) out[base + t] = res;
+}
+
+// ---------------------------------------------------------------------------
+// two-lane path: lanes 2c and 2c+1 share coordinate c of the wave's 32; lane h
+// holds rows h, h+2, h+4, ... (H values, P = 2H slots, n in (P/2, P]).
+//  1. NaNs are counted (only if the wave saw one) and mapped to +inf, so the
+//     compare-exchanges are plain v_min/v_max; pads are +inf (median: split
+//     -inf / +inf so the middle lands on fixed slots H-1, H).
+//  2. each lane sorts its H values (odd-even merge network);
+//  3. one cross-lane bitonic step through DPP (quad_perm [1,0,3,2]): the even
+//     lane keeps min(a_i, b_{H-1-i}), the odd lane max(b_i, a_{H-1-i}) -- both
+//     bitonic -- and both lanes finish with the same half-cleaner cascade, so
+//     the even lane ends with merged slots 0..H-1 and the odd lane H..2H-1;
+//  4. trimmed mean: the even lane sums its kept slots in ascending order, hands
+//     the partial to the odd lane (DPP), which continues -- the sequential
+//     ascending-order fp32 sum of numpy, bit for bit.
+// Half the registers of the one-lane path -> ~2x the waves in flight.
+// Requires ldx*4 < 2^31 (the odd lane's row offset is a 32-bit lane offset).
+// ---------------------------------------------------------------------------
+template <int H, int MODE, int NX, int BX, int BS = 256>
+__global__ void __launch_bounds__(BS) select2_kernel(const float* __restrict__ X, int n_rt, int64_t d,
+                                                     int64_t ldx, int lo_rt, int hi_rt, float* __restrict__ out) {
+  constexpr int P = 2 * H;
+  constexpr bool kExactN = NX > 0;
+  constexpr bool kExactB = kExactN && BX >= 0;
+  const int n = kExactN ? NX : n_rt;
+  const int lo = kExactB ? BX : lo_rt;
+  const int hi = kExactB ? NX - BX : hi_rt;
+  const unsigned h = threadIdx.x & 1u;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * (BS / 2);
+  const int64_t rem = d - base;
+  const unsigned jl0 = threadIdx.x >> 1;
+  const unsigned last = rem < BS / 2 ? static_cast<unsigned>(rem - 1) : static_cast<unsigned>(BS / 2 - 1);
+  const unsigned jl = jl0 < last ? jl0 : last;
+  const int64_t ldb = ldx * 4;
+  const unsigned off_pair = static_cast<unsigned>(h * ldb) + jl * 4u;  // row 2i+h
+  const unsigned off_even = jl * 4u;                                     // row 2i (clamped rows)
+  const char* xb = reinterpret_cast<const char*>(X + base);
+  const int k_bottom = (MODE == kMedian) ? (P - n) / 2 : 0;
+
+  float v[H];
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const int r0 = 2 * i;
+    float x;
+    if (r0 + 1 < n) {                       // both rows of the pair are real
+      x = ldrow(xb + r0 * ldb, off_pair);
+    } else {                                // tail: clamp to a real row, pad later
+      const int rc = r0 < n ? r0 : n - 1;
+      x = ldrow(xb + rc * ldb, off_even);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int row = r0 + static_cast<int>(h);
+    const bool real = row < n;
+    m = (i == 0) ? x : (real ? __builtin_elementwise_maximum(m, x) : m);
+    const float pad = (row - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
+    v[i] = real ? x : pad;
+  }
+  // NaN bookkeeping (rare; wave-uniform branch)
+  int nan_cnt = 0;
+  const bool lane_nan = __builtin_isnan(m);
+  if (__builtin_amdgcn_ballot_w64(lane_nan) != 0) {
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      nan_cnt += __builtin_isnan(v[i]) ? 1 : 0;
+      v[i] = __builtin_fminf(v[i], __builtin_inff());  // NaN -> +inf
+    }
+  }
+  nan_cnt += __builtin_bit_cast(int, swap_adjacent(__builtin_bit_cast(float, nan_cnt)));
+
+  network_plain<H, H, 0, H, kNetSort>(v);
+  float w[H];
+#pragma unroll
+  for (int i = 0; i < H / 2; ++i) {
+    const int k = H - 1 - i;
+    const float pi = swap_adjacent(v[k]);
+    const float pk = swap_adjacent(v[i]);
+    w[i] = h ? __builtin_fmaxf(v[i], pi) : __builtin_fminf(v[i], pi);
+    w[k] = h ? __builtin_fmaxf(v[k], pk) : __builtin_fminf(v[k], pk);
+  }
+  network_plain<H, H, 0, H, kNetMerge>(w);
+
+  float res;
+  bool writer;
+  if constexpr (MODE == kMedian) {
+    const float t = h ? w[0] : w[H - 1];
+    const float other = swap_adjacent(t);
+    res = (n & 1) ? t : (t + other) * 0.5f;
+    if (nan_cnt > 0) res = qnan();
+    writer = h == 0;
+  } else {
+    const int e_hi = hi < H ? hi : H;
+    const int o_lo = (lo > H ? lo : H) - H;
+    const int o_hi = hi - H;
+    float acc = 0.f;
+#pragma unroll
+    for (int p = 0; p < H; ++p) {
+      if (p >= lo && p < e_hi) {
+        if constexpr (!kExactB) asm volatile("");
+        acc += w[p];
+      }
+    }
+    float acc2 = swap_adjacent(acc);
+#pragma unroll
+    for (int p = 0; p < H; ++p) {
+      if (p >= o_lo && p < o_hi) {
+        if constexpr (!kExactB) asm volatile("");
+        acc2 += w[p];
+      }
+    }
+    res = acc2 / static_cast<float>(hi - lo);
+    if (nan_cnt > n - hi) res = qnan();
+    writer = h == 1;
+  }
+  if (writer && jl0 < rem) out[base + jl0] = res;
 }
 
 // ---------------------------------------------------------------------------
@@ -204,30 +355,77 @@ __global__ void __launch_bounds__(256) select_lds_kernel(const float* __restrict
   }
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e != nullptr && e[0] != 0) ? atoi(e) : dflt;
+}
+
+// Variant selection.  Defaults are the measured-fastest; the
+// SRA_SELECT (1 = one-lane, 2 = two-lane) and SRA_BS (block size) environment
+// variables exist for A/B measurements only.
 template <int MODE>
 static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, int hi, float* out,
                          hipStream_t s) {
-  const int64_t blocks = cdiv(d, 256);
+  static const int force = env_int("SRA_SELECT", 0);
+  static const int bs_env = env_int("SRA_BS", 0);
   const int P = static_cast<int>(cdiv(n, 16) * 16);
-#define SRA_SEL_CASE(PP)                                                                              \
-  case PP:                                                                                            \
-    hipLaunchKernelGGL((select_reg_kernel<PP, MODE>), dim3(blocks), dim3(256), 0, s, X, n, d, ldx, lo, \
-                       hi, out);                                                                      \
-    return launch_status("select_reg_kernel");
+  const bool two_lane_ok = ldx * 4 < (int64_t(1) << 31);
+  const bool trim128 = MODE == kTrimmed && n == 128 && lo == 12 && hi == 116;
+  const bool trim100 = MODE == kTrimmed && n == 100 && lo == 10 && hi == 90;
+
+  if (force == 2 && two_lane_ok && n > 32 && n <= 256) {
+    const int bs = bs_env == 1024 ? 1024 : 256;
+#define SRA_SEL2(HH, NXX, BXX)                                                                                   \
+  do {                                                                                                           \
+    if (bs == 1024)                                                                                              \
+      hipLaunchKernelGGL((select2_kernel<HH, MODE, NXX, BXX, 1024>), dim3(cdiv(d, 512)), dim3(1024), 0, s, X, n, d, \
+                         ldx, lo, hi, out);                                                                      \
+    else                                                                                                         \
+      hipLaunchKernelGGL((select2_kernel<HH, MODE, NXX, BXX, 256>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, \
+                         ldx, lo, hi, out);                                                                      \
+    return launch_status("select2_kernel");                                                                      \
+  } while (0)
+    if (trim128) SRA_SEL2(64, 128, 12);
+    if (MODE == kMedian && n == 128) SRA_SEL2(64, 128, -1);
+    if (n <= 64) SRA_SEL2(32, 0, -1);
+    if (n <= 128) SRA_SEL2(64, 0, -1);
+    SRA_SEL2(128, 0, -1);
+#undef SRA_SEL2
+  }
   if (n <= 128) {
+    const int bs = bs_env == 768 ? 768 : 256;
+#define SRA_SEL1(PP, NXX, BXX)                                                                                   \
+  do {                                                                                                           \
+    if (bs == 768)                                                                                               \
+      hipLaunchKernelGGL((select_reg_kernel<PP, MODE, NXX, BXX, 768>), dim3(cdiv(d, 768)), dim3(768), 0, s, X, n, \
+                         d, ldx, lo, hi, out);                                                                   \
+    else                                                                                                         \
+      hipLaunchKernelGGL((select_reg_kernel<PP, MODE, NXX, BXX, 256>), dim3(cdiv(d, 256)), dim3(256), 0, s, X, n, \
+                         d, ldx, lo, hi, out);                                                                   \
+    return launch_status("select_reg_kernel");                                                                   \
+  } while (0)
+    if (trim128) SRA_SEL1(128, 128, 12);
+    if (trim100) SRA_SEL1(112, 100, 10);
+    if (MODE == kMedian && n == 128) SRA_SEL1(128, 128, -1);
+    if (MODE == kMedian && n == 100) SRA_SEL1(112, 100, -1);
     switch (P) {
-      SRA_SEL_CASE(16)
-      SRA_SEL_CASE(32)
-      SRA_SEL_CASE(48)
-      SRA_SEL_CASE(64)
-      SRA_SEL_CASE(80)
-      SRA_SEL_CASE(96)
-      SRA_SEL_CASE(112)
-      SRA_SEL_CASE(128)
+      case 16: SRA_SEL1(16, 0, -1);
+      case 32: SRA_SEL1(32, 0, -1);
+      case 48: SRA_SEL1(48, 0, -1);
+      case 64: SRA_SEL1(64, 0, -1);
+      case 80: SRA_SEL1(80, 0, -1);
+      case 96: SRA_SEL1(96, 0, -1);
+      case 112: SRA_SEL1(112, 0, -1);
+      case 128: SRA_SEL1(128, 0, -1);
       default: break;
     }
+#undef SRA_SEL1
   }
-#undef SRA_SEL_CASE
+  if (two_lane_ok && n > 128 && n <= 256) {
+    hipLaunchKernelGGL((select2_kernel<128, MODE, 0, -1, 256>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, ldx,
+                       lo, hi, out);
+    return launch_status("select2_kernel");
+  }
   const int pn = next_pow2(n);
   SRA_REQUIRE(pn <= kLdsFloats / 4, SRA_ERR_UNSUPPORTED, "k-select supports N <= %d (got %d)", kLdsFloats / 4, n);
   const int tile = kLdsFloats / pn;

@@ -69,57 +69,116 @@ __device__ __forceinline__ void ce(float& a, float& b) {
 // ---------------------------------------------------------------------------
 // Sorting-network planner (all constexpr).
 //
-// Batcher's odd-even merge sort on P2 = 2^k slots.  Slots [PR, P2) hold a
-// compile-time NaN (they sort last), so the forward pass folds every CE that
-// touches them: (x, NaN) is a no-op, (NaN, x) is a register move.  A backward
-// pass then keeps only the cone of the requested output slots [OLO, OHI): a CE
-// with one live output becomes a single min or max, one with none is dropped.
-// The result is an op list whose indices are immediates after expansion.
+// Two base networks on P2 = 2^k slots:
+//   kNetSort  — Batcher's odd-even merge sort (sorts anything);
+//   kNetMerge — bitonic half-cleaner cascade (sorts a bitonic sequence).
+// Slots [PR, P2) hold a compile-time "top" value (sorts after everything), so
+// the forward pass folds every CE that touches them: (x, top) is a no-op,
+// (top, x) is a register move.  A backward pass then keeps only the cone of
+// the requested output slots [OLO, OHI): a CE with one live output becomes a
+// single min or max, one with none is dropped.  The resulting op list is
+// expanded with immediate register indices.
 // ---------------------------------------------------------------------------
 enum NetOpKind : int { kOpCE = 0, kOpMin = 1, kOpMax = 2, kOpMove = 3 };
+enum NetKind : int { kNetSort = 0, kNetMerge = 1 };
 
-template <int P2>
-struct OddEvenFull {
+template <int P2, int KIND>
+struct BaseNet {
+  template <typename F>
+  static constexpr void each(F&& f) {
+    if constexpr (KIND == kNetSort) {
+      // depth-first Batcher odd-even merge sort: sort(lo half), sort(hi half),
+      // merge.  Same comparators as the stage-major form, but the first rows'
+      // sub-sort only reads the first loads, so a wave starts sorting while
+      // the rest of its column is still in flight.
+      sort_hybrid(f, 0, P2);
+    } else {
+      for (int s = P2 / 2; s >= 1; s >>= 1)
+        for (int i = 0; i < P2; ++i)
+          if ((i & s) == 0) f(i, i + s);
+    }
+  }
+  template <typename F>
+  static constexpr void merge_rec(F& f, int lo, int n, int r) {
+    const int step = r * 2;
+    if (step < n) {
+      merge_rec(f, lo, n, step);
+      merge_rec(f, lo + r, n, step);
+      for (int i = lo + r; i + r < lo + n; i += step) f(i, i + r);
+    } else {
+      f(lo, lo + r);
+    }
+  }
+  // stage-major odd-even merge of the two sorted halves of [lo, lo+n)
+  template <typename F>
+  static constexpr void merge_stages(F& f, int lo, int n) {
+    const int p = n / 2;
+    for (int k = p; k >= 1; k >>= 1)
+      for (int j = k % p; j + k < n; j += 2 * k)
+        for (int i = 0; i < k && i + j + k < n; ++i) f(lo + i + j, lo + i + j + k);
+  }
+  // stage-major odd-even merge sort of [lo, lo+n)
+  template <typename F>
+  static constexpr void sort_stages(F& f, int lo, int n) {
+    for (int p = 1; p < n; p <<= 1)
+      for (int k = p; k >= 1; k >>= 1)
+        for (int j = k % p; j + k < n; j += 2 * k)
+          for (int i = 0; i < k && i + j + k < n; ++i)
+            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) f(lo + i + j, lo + i + j + k);
+  }
+  // depth-first over blocks of kBlock rows (a wave starts sorting its first
+  // rows while later loads are in flight), stage-major inside a block and in
+  // each merge (consecutive comparators independent -> wide asm groups and
+  // few dependent asm boundaries)
+  static constexpr int kBlock = 32;
+  template <typename F>
+  static constexpr void sort_hybrid(F& f, int lo, int n) {
+    if (n <= kBlock) {
+      sort_stages(f, lo, n);
+      return;
+    }
+    sort_hybrid(f, lo, n / 2);
+    sort_hybrid(f, lo + n / 2, n / 2);
+    merge_stages(f, lo, n);
+  }
+  template <typename F>
+  static constexpr void sort_rec(F& f, int lo, int n) {
+    if (n > 1) {
+      const int m = n / 2;
+      sort_rec(f, lo, m);
+      sort_rec(f, lo + m, m);
+      merge_rec(f, lo, n, 1);
+    }
+  }
   static constexpr int count() {
     int c = 0;
-    for (int p = 1; p < P2; p <<= 1)
-      for (int k = p; k >= 1; k >>= 1)
-        for (int j = k % p; j + k < P2; j += 2 * k)
-          for (int i = 0; i < k && i + j + k < P2; ++i)
-            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) ++c;
-    return c;
+    each([&](int, int) { ++c; });
+    return c > 0 ? c : 1;
   }
-  static constexpr int N = count() > 0 ? count() : 1;
+  static constexpr int N = count();
 };
 
-template <int P2, int PR, int OLO, int OHI>
+template <int P2, int PR, int OLO, int OHI, int KIND>
 struct NetPlanData {
-  static constexpr int NF = OddEvenFull<P2>::N;
+  static constexpr int NF = BaseNet<P2, KIND>::N;
   int n = 0;
   short kind[NF] = {};
   short a[NF] = {};
   short b[NF] = {};
   constexpr NetPlanData() {
-    // forward: full network with constant-NaN folding
     short fk[NF] = {}, fa[NF] = {}, fb[NF] = {};
     bool cst[P2] = {};
     for (int i = 0; i < P2; ++i) cst[i] = i >= PR;
     int m = 0;
-    for (int p = 1; p < P2; p <<= 1)
-      for (int k = p; k >= 1; k >>= 1)
-        for (int j = k % p; j + k < P2; j += 2 * k)
-          for (int i = 0; i < k && i + j + k < P2; ++i)
-            if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
-              const int x = i + j, y = i + j + k;
-              if (cst[y]) continue;                       // (v, NaN): already ordered
-              if (cst[x]) {                               // (NaN, v): move v down
-                fk[m] = kOpMove; fa[m] = x; fb[m] = y; ++m;
-                cst[x] = false; cst[y] = true;
-                continue;
-              }
-              fk[m] = kOpCE; fa[m] = x; fb[m] = y; ++m;
-            }
-    // backward: keep the cone of the requested outputs
+    BaseNet<P2, KIND>::each([&](int x, int y) {
+      if (cst[y]) return;                           // (v, top): already ordered
+      if (cst[x]) {                                 // (top, v): move v down
+        fk[m] = kOpMove; fa[m] = x; fb[m] = y; ++m;
+        cst[x] = false; cst[y] = true;
+        return;
+      }
+      fk[m] = kOpCE; fa[m] = x; fb[m] = y; ++m;
+    });
     bool need[P2] = {};
     for (int i = OLO; i < OHI; ++i) need[i] = true;
     bool keep[NF] = {};
@@ -139,13 +198,36 @@ struct NetPlanData {
     }
     for (int q = 0; q < m; ++q)
       if (keep[q]) { kind[n] = fk[q]; a[n] = fa[q]; b[n] = fb[q]; ++n; }
+    // greedy groups of up to kGroup consecutive, mutually independent CEs
+    // (one inline-asm statement each; other ops are groups of one)
+    int q = 0;
+    while (q < n) {
+      gstart[ngroups] = q;
+      int len = 1;
+      if (kind[q] == kOpCE) {
+        while (q + len < n && len < kGroup && kind[q + len] == kOpCE) {
+          bool clash = false;
+          for (int t = q; t < q + len; ++t)
+            if (a[t] == a[q + len] || a[t] == b[q + len] || b[t] == a[q + len] || b[t] == b[q + len]) clash = true;
+          if (clash) break;
+          ++len;
+        }
+      }
+      glen[ngroups] = len;
+      ++ngroups;
+      q += len;
+    }
   }
+  static constexpr int kGroup = 4;
+  int ngroups = 0;
+  short gstart[NF] = {};
+  short glen[NF] = {};
 };
 
-// evaluated once per (P2, PR, OLO, OHI)
-template <int P2, int PR, int OLO, int OHI>
+// evaluated once per instantiation
+template <int P2, int PR, int OLO, int OHI, int KIND = kNetSort>
 struct NetPlan {
-  static constexpr NetPlanData<P2, PR, OLO, OHI> value{};
+  static constexpr NetPlanData<P2, PR, OLO, OHI, KIND> value{};
 };
 
 // One compare-exchange as an indivisible pair (lo into a fresh register, hi in
@@ -155,6 +237,81 @@ __device__ __forceinline__ void ce_pair(float& a, float& b) {
   float lo;
   asm("v_min_f32 %0, %2, %1\n\tv_maximum3_f32 %1, %2, %1, %1" : "=&v"(lo), "+v"(b) : "v"(a));
   a = lo;
+}
+
+// Up to four independent NaN-free compare-exchanges in ONE asm statement:
+// lo into a fresh register, hi in place.  The asm keeps the CE order (and
+// therefore the live set at ~P values); grouping keeps the compiler's
+// conservative post-asm hazard padding (one s_nop per dependent asm boundary)
+// to one per group.  IEEE-754-2019 minimum/maximum need no canonicalised
+// operands; callers map NaN to +inf beforehand.
+__device__ __forceinline__ void ce_asm1(float& a0, float& b0) {
+  float l0;
+  asm("v_minimum3_f32 %0, %2, %1, %1\n\tv_maximum3_f32 %1, %2, %1, %1" : "=&v"(l0), "+v"(b0) : "v"(a0));
+  a0 = l0;
+}
+__device__ __forceinline__ void ce_asm2(float& a0, float& b0, float& a1, float& b1) {
+  float l0, l1;
+  asm("v_minimum3_f32 %0, %4, %2, %2\n\tv_maximum3_f32 %2, %4, %2, %2\n\t"
+      "v_minimum3_f32 %1, %5, %3, %3\n\tv_maximum3_f32 %3, %5, %3, %3"
+      : "=&v"(l0), "=&v"(l1), "+v"(b0), "+v"(b1) : "v"(a0), "v"(a1));
+  a0 = l0; a1 = l1;
+}
+__device__ __forceinline__ void ce_asm3(float& a0, float& b0, float& a1, float& b1, float& a2, float& b2) {
+  float l0, l1, l2;
+  asm("v_minimum3_f32 %0, %6, %3, %3\n\tv_maximum3_f32 %3, %6, %3, %3\n\t"
+      "v_minimum3_f32 %1, %7, %4, %4\n\tv_maximum3_f32 %4, %7, %4, %4\n\t"
+      "v_minimum3_f32 %2, %8, %5, %5\n\tv_maximum3_f32 %5, %8, %5, %5"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "+v"(b0), "+v"(b1), "+v"(b2) : "v"(a0), "v"(a1), "v"(a2));
+  a0 = l0; a1 = l1; a2 = l2;
+}
+__device__ __forceinline__ void ce_asm4(float& a0, float& b0, float& a1, float& b1, float& a2, float& b2,
+                                        float& a3, float& b3) {
+  float l0, l1, l2, l3;
+  asm("v_minimum3_f32 %0, %8, %4, %4\n\tv_maximum3_f32 %4, %8, %4, %4\n\t"
+      "v_minimum3_f32 %1, %9, %5, %5\n\tv_maximum3_f32 %5, %9, %5, %5\n\t"
+      "v_minimum3_f32 %2, %10, %6, %6\n\tv_maximum3_f32 %6, %10, %6, %6\n\t"
+      "v_minimum3_f32 %3, %11, %7, %7\n\tv_maximum3_f32 %7, %11, %7, %7"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3));
+  a0 = l0; a1 = l1; a2 = l2; a3 = l3;
+}
+
+template <typename Plan, int G, int P2>
+__device__ __forceinline__ void net_group(float (&v)[P2]) {
+  // every index is forced through a constexpr so it becomes an immediate
+  // register number (a plain use of the table would be a runtime load)
+  constexpr int q = Plan::value.gstart[G], len = Plan::value.glen[G];
+  constexpr int kd = Plan::value.kind[q];
+  constexpr int a0 = Plan::value.a[q], b0 = Plan::value.b[q];
+  constexpr int a1 = len > 1 ? Plan::value.a[q + 1] : 0, b1 = len > 1 ? Plan::value.b[q + 1] : 0;
+  constexpr int a2 = len > 2 ? Plan::value.a[q + 2] : 0, b2 = len > 2 ? Plan::value.b[q + 2] : 0;
+  constexpr int a3 = len > 3 ? Plan::value.a[q + 3] : 0, b3 = len > 3 ? Plan::value.b[q + 3] : 0;
+  if constexpr (kd == kOpCE) {
+    if constexpr (len == 1) ce_asm1(v[a0], v[b0]);
+    else if constexpr (len == 2) ce_asm2(v[a0], v[b0], v[a1], v[b1]);
+    else if constexpr (len == 3) ce_asm3(v[a0], v[b0], v[a1], v[b1], v[a2], v[b2]);
+    else ce_asm4(v[a0], v[b0], v[a1], v[b1], v[a2], v[b2], v[a3], v[b3]);
+  } else if constexpr (kd == kOpMin) {
+    v[a0] = __builtin_elementwise_minimum(v[a0], v[b0]);
+  } else if constexpr (kd == kOpMax) {
+    v[b0] = __builtin_elementwise_maximum(v[a0], v[b0]);
+  } else {
+    v[a0] = v[b0];
+  }
+}
+
+template <typename Plan, int P2, size_t... G>
+__device__ __forceinline__ void net_run_groups(float (&v)[P2], std::index_sequence<G...>) {
+  (net_group<Plan, G>(v), ...);
+}
+
+// NaN-free sort of (the requested slots of) v[0..P2): slots [PR, P2) are
+// implicit +inf; on return slots [OLO, OHI) hold ascending order statistics.
+template <int P2, int PR, int OLO, int OHI, int KIND = kNetSort>
+__device__ __forceinline__ void network_fast(float (&v)[P2]) {
+  using Plan = NetPlan<P2, PR, OLO, OHI, KIND>;
+  if constexpr (P2 > 1) net_run_groups<Plan>(v, std::make_index_sequence<Plan::value.ngroups>{});
 }
 
 template <typename Plan, int Q, int P2>
@@ -172,12 +329,52 @@ __device__ __forceinline__ void net_run(float (&v)[P2], std::index_sequence<Q...
 }
 
 // Sort (the requested slots of) v[0..P2): slots [0, PR) are live values,
-// [PR, P2) are implicit NaN; on return slots [OLO, OHI) hold the ascending
-// order statistics (NaN last).  P2 must be a power of two >= PR.
+// [PR, P2) are implicit "top" values; on return slots [OLO, OHI) hold the
+// ascending order statistics (NaN last).  P2 must be a power of two >= PR.
 template <int P2, int PR, int OLO, int OHI>
 __device__ __forceinline__ void sort_network(float (&v)[P2]) {
-  using Plan = NetPlan<P2, PR, OLO, OHI>;
+  using Plan = NetPlan<P2, PR, OLO, OHI, kNetSort>;
   if constexpr (P2 > 1) net_run<Plan>(v, std::make_index_sequence<Plan::value.n>{});
+}
+
+// Sort a bitonic sequence v[0..P2) ascending (bitonic half-cleaner cascade).
+template <int P2>
+__device__ __forceinline__ void bitonic_merge(float (&v)[P2]) {
+  using Plan = NetPlan<P2, P2, 0, P2, kNetMerge>;
+  if constexpr (P2 > 1) net_run<Plan>(v, std::make_index_sequence<Plan::value.n>{});
+}
+
+// Plain (NaN-free) variants: lo = v_min_f32, hi = v_max_f32.  Used after NaNs
+// have been mapped to +inf (their count is tracked separately).
+__device__ __forceinline__ void ce_pair_plain(float& a, float& b) {
+  float lo;
+  asm("v_min_f32 %0, %2, %1\n\tv_max_f32 %1, %2, %1" : "=&v"(lo), "+v"(b) : "v"(a));
+  a = lo;
+}
+
+template <typename Plan, int Q, int P2>
+__device__ __forceinline__ void net_op_plain(float (&v)[P2]) {
+  constexpr int kd = Plan::value.kind[Q], x = Plan::value.a[Q], y = Plan::value.b[Q];
+  if constexpr (kd == kOpCE) ce_pair_plain(v[x], v[y]);
+  else if constexpr (kd == kOpMin) v[x] = __builtin_fminf(v[x], v[y]);
+  else if constexpr (kd == kOpMax) v[y] = __builtin_fmaxf(v[x], v[y]);
+  else v[x] = v[y];
+}
+
+template <typename Plan, int P2, size_t... Q>
+__device__ __forceinline__ void net_run_plain(float (&v)[P2], std::index_sequence<Q...>) {
+  (net_op_plain<Plan, Q>(v), ...);
+}
+
+template <int P2, int PR, int OLO, int OHI, int KIND>
+__device__ __forceinline__ void network_plain(float (&v)[P2]) {
+  using Plan = NetPlan<P2, PR, OLO, OHI, KIND>;
+  if constexpr (P2 > 1) net_run_plain<Plan>(v, std::make_index_sequence<Plan::value.n>{});
+}
+
+// DPP lane exchange with the neighbour lane (quad_perm [1,0,3,2]: 2c <-> 2c+1)
+__device__ __forceinline__ float swap_adjacent(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ float qnan() { return __builtin_nanf(""); }
