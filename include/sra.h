@@ -72,6 +72,54 @@ int sra_median_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* out
 int sra_trimmed_mean_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t b, float* out,
                          void* stream);
 
+
+/* ------------------------------------------------------------------------ */
+/* Pairwise L2 / Krum (k2 MFMA Gram + k3 client-space scoring)               */
+/* ------------------------------------------------------------------------ */
+
+/* Workspace for sra_gram_f32 (partial-Gram slab), in bytes. */
+int sra_gram_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
+
+/* G (n x n, fp64, row-major, symmetric) = centred Gram of the clients:
+ * G_ij = sum_k (X[i,k] - mu_k)(X[j,k] - mu_k) with mu a per-coordinate shift,
+ * so ||x_i - x_j||^2 = G_ii + G_jj - 2 G_ij.  fp32 MFMA, fp64 reduction.
+ * 1 <= n <= 256.  Feeds krum_ (src/robust_estimator.py:234-244). */
+int sra_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes,
+                 void* stream);
+
+/* Workspace for sra_krum_select_f32, in bytes. */
+int sra_krum_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
+
+/* `rounds` Krum selections with f fixed over a shrinking set:
+ *  round t scores every remaining client by the numpy-pairwise fp32 sum of
+ *  its (n_remaining - f - 2) smallest distances (Python slice semantics),
+ *  picks the first minimum and removes it; order[t] = its client index.
+ *  rounds = 1 is robust_estimator.krum (src/robust_estimator.py:246-249);
+ *  rounds = theta is the selection of bulyan(aggsubfunc='krum') (:286-296).
+ *  scores (optional, n floats) receive round 0's scores = krum_'s metric. */
+int sra_krum_select_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t rounds,
+                        int32_t* order, float* scores, void* ws, size_t ws_bytes, void* stream);
+
+/* Same selection from a precomputed Gram G (e.g. summed over GPUs);
+ * ws >= 12*n*n bytes. */
+int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t rounds, int32_t* order, float* scores,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* out[r, :] = X[rows[r], :] for r < nrows (rows is a device int32 array). */
+int sra_gather_rows_f32(const float* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows, float* out,
+                        int64_t ldo, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Median-of-means bucketing (k5)                                            */
+/* ------------------------------------------------------------------------ */
+
+/* out[b, :] = mean of X rows [b*bucket_size, min((b+1)*bucket_size, n)),
+ * sequential fp32 sum / count, b < nbuckets.  SRA_ERR_EMPTY_BUCKET if a bucket
+ * would be empty (the reference then raises ValueError).
+ * Replaces the bucketing of src/robust_estimator.py:135-140, 210-216, 251-256. */
+int sra_bucket_mean_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size, int32_t nbuckets,
+                        float* out, int64_t ldo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

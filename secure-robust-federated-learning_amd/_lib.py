@@ -64,6 +64,13 @@ _SIGS = {
     "sra_average_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr],
     "sra_median_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr],
     "sra_trimmed_mean_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr],
+    "sra_gram_workspace_bytes": [_i64, _i64, ctypes.POINTER(_sz)],
+    "sra_gram_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr, _sz, _ptr],
+    "sra_krum_workspace_bytes": [_i64, _i64, ctypes.POINTER(_sz)],
+    "sra_krum_select_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_krum_from_gram": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_gather_rows_f32": [_ptr, _i64, _i64, _ptr, _i32, _ptr, _i64, _ptr],
+    "sra_bucket_mean_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _i64, _ptr],
 }
 _RESTYPES = {"sra_last_error": ctypes.c_char_p}
 
@@ -112,6 +119,13 @@ def load(path=None):
 
 def last_error():
     return load().sra_last_error().decode(errors="replace")
+
+
+def query_bytes(name, *args):
+    """Call a ``*_workspace_bytes`` query and return the size."""
+    out = _sz(0)
+    call(name, *args, ctypes.byref(out))
+    return int(out.value)
 
 
 def call(name, *args):

@@ -1,0 +1,266 @@
+// k3 — Krum scoring in client space (N x N), from the centred Gram of k2.
+//
+// Replaces the O(N^2 d) Python double loop of krum_ (src/robust_estimator.py:
+// 234-244), krum's argmin (:246-249) and the theta selection rounds of
+// bulyan(aggsubfunc='krum') (:286-296), which call krum on the remaining set
+// with f fixed and delete the chosen client by identity.
+//
+//   d_ij  = fp32(sqrt(max(G_ii + G_jj - 2 G_ij, 0)))      (fp64 arithmetic)
+//   score = numpy pairwise fp32 sum of the m smallest d_ij, j != i, j alive,
+//           in ascending order, m = Python-slice count of (n_alive - f - 2)
+//   pick  = first index (in client order) of the minimum score
+//
+// Each row is sorted once (bitonic in LDS, ties by j); a round then compacts
+// the first m alive entries of each row and reduces them in numpy's order, so
+// a theta-round Bulyan-Krum costs theta * N^2 instead of theta * N^2 log N.
+// Everything runs in one workgroup: N-space work is microseconds and needs no
+// host synchronisation between rounds.
+#include "sra_common.hpp"
+
+namespace sra {
+
+constexpr int kMaxClients = 256;
+
+// numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src) for
+// float32, n elements at a[0..n): < 8 sequential from 0; <= 128 eight
+// accumulators then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail;
+// otherwise split at n/2 rounded down to a multiple of 8.
+template <int DEPTH>
+__device__ float np_pairwise_f32(const float* a, int n) {
+  if (n < 8) {
+    float res = 0.f;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  if (n <= 128 || DEPTH == 0) {
+    float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+      r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+      r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+    }
+    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  if constexpr (DEPTH > 0) {
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise_f32<DEPTH - 1>(a, n2) + np_pairwise_f32<DEPTH - 1>(a + n2, n - n2);
+  }
+  return 0.f;
+}
+
+// distance matrix (fp32) from the fp64 Gram
+__global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __restrict__ D) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * n) return;
+  const int i = e / n, j = e - (e / n) * n;
+  double sq = G[(int64_t)i * n + i] + G[(int64_t)j * n + j] - 2.0 * G[e];
+  if (i == j) sq = 0.0;
+  D[e] = static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
+}
+
+// Sort every row's off-diagonal distances ascending (ties by j): one workgroup
+// per row, bitonic network in LDS over next_pow2(n-1) slots.
+__global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restrict__ D, int n,
+                                                           float* __restrict__ S, int* __restrict__ J) {
+  __shared__ float kv[kMaxClients];
+  __shared__ int kj[kMaxClients];
+  const int i = blockIdx.x;
+  const int m = n - 1;
+  int pn = 1;
+  while (pn < m) pn <<= 1;
+  for (int p = threadIdx.x; p < pn; p += blockDim.x) {
+    if (p < m) {
+      const int j = p < i ? p : p + 1;
+      kv[p] = D[(int64_t)i * n + j];
+      kj[p] = j;
+    } else {
+      kv[p] = __builtin_inff();
+      kj[p] = 0x7fffffff;
+    }
+  }
+  __syncthreads();
+  for (int k = 2; k <= pn; k <<= 1) {
+    for (int s = k >> 1; s > 0; s >>= 1) {
+      for (int h = threadIdx.x; h < pn / 2; h += blockDim.x) {
+        const int a = (h / s) * (2 * s) + (h % s);
+        const int b = a + s;
+        const bool up = (a & k) == 0;
+        const float va = kv[a], vb = kv[b];
+        const int ja = kj[a], jb = kj[b];
+        // order (value, j); NaN sorts as the largest value
+        const bool a_gt = (va != va) ? !((vb != vb) && ja < jb)
+                                     : ((vb != vb) ? false : (va > vb || (va == vb && ja > jb)));
+        if (a_gt == up) {
+          kv[a] = vb; kv[b] = va;
+          kj[a] = jb; kj[b] = ja;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int p = threadIdx.x; p < m; p += blockDim.x) {
+    S[(int64_t)i * n + p] = kv[p];
+    J[(int64_t)i * n + p] = kj[p];
+  }
+}
+
+// Python slice length of a[:size_] for a length-`len` array.
+__device__ __forceinline__ int slice_count(int size_, int len) {
+  if (size_ >= 0) return size_ < len ? size_ : len;
+  const int c = len + size_;
+  return c > 0 ? c : 0;
+}
+
+// `rounds` Krum selections over a shrinking alive set (rounds = 1: plain krum).
+// order[t] = client chosen in round t; scores (round 0, all N) optional.
+__global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restrict__ S, const int* __restrict__ J,
+                                                           int n, int f, int rounds, int* __restrict__ order,
+                                                           float* __restrict__ scores0, int* __restrict__ status) {
+  __shared__ unsigned char alive[kMaxClients];
+  __shared__ float score[kMaxClients];
+  __shared__ float gath[16][kMaxClients];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int nwaves = blockDim.x >> 6;
+  for (int i = tid; i < n; i += blockDim.x) alive[i] = 1;
+  __syncthreads();
+  for (int t = 0; t < rounds; ++t) {
+    const int nr = n - t;
+    const int m = slice_count(nr - f - 2, nr - 1);
+    for (int i = wave; i < n; i += nwaves) {
+      if (!alive[i]) continue;  // wave-uniform
+      // compact the first m alive entries of sorted row i into gath[wave]
+      int c = 0;
+      for (int p0 = 0; p0 < n - 1 && c < m; p0 += 64) {
+        const int p = p0 + lane;
+        const bool ok = p < n - 1 && alive[J[(int64_t)i * n + p]];
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
+        const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
+        if (ok && c + pre < m) gath[wave][c + pre] = S[(int64_t)i * n + p];
+        c += __builtin_popcountll(bal);
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) score[i] = np_pairwise_f32<3>(gath[wave], m);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // np.argmin: first minimum; a NaN is the minimum (first NaN wins)
+      int best = -1;
+      float bv = 0.f;
+      for (int i = 0; i < n; ++i) {
+        if (!alive[i]) continue;
+        const float v = score[i];
+        if (best < 0) { best = i; bv = v; if (v != v) break; continue; }
+        if (v != v) { best = i; break; }
+        if (v < bv) { best = i; bv = v; }
+      }
+      order[t] = best;
+      if (best >= 0) alive[best] = 0;
+      if (best < 0 && status) *status = 1;
+    }
+    if (t == 0 && scores0) {
+      __syncthreads();
+      for (int i = tid; i < n; i += blockDim.x) scores0[i] = score[i];
+    }
+    __syncthreads();
+  }
+}
+
+// out[:] = X[order[sel], :] (the chosen client's row), and optional gathered rows
+__global__ void gather_rows_kernel(const float* __restrict__ X, int64_t d, int64_t ldx, const int* __restrict__ order,
+                                   int nrows, float* __restrict__ out, int64_t ldo) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int r = blockIdx.y;
+  if (j >= d || r >= nrows) return;
+  const int src = order[r];
+  out[r * ldo + j] = X[static_cast<int64_t>(src) * ldx + j];
+}
+
+size_t krum_workspace_bytes(int n, int64_t d);
+size_t gram_workspace_bytes(int n, int64_t d);
+int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes, hipStream_t s);
+
+// workspace layout: [G fp64 n*n][D n*n][S n*n][J n*n][gram slab]
+size_t krum_workspace_bytes(int n, int64_t d) {
+  const size_t nn = static_cast<size_t>(n) * n;
+  return 256 + nn * 8 + nn * 4 * 3 + gram_workspace_bytes(n, d);
+}
+
+int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int* order, float* scores0,
+                                 char* ws, hipStream_t s) {
+  const size_t nn = static_cast<size_t>(n) * n;
+  float* D = reinterpret_cast<float*>(ws);
+  float* S = D + nn;
+  int* J = reinterpret_cast<int*>(S + nn);
+  hipLaunchKernelGGL(krum_dist_kernel, dim3(cdiv(n * n, 256)), dim3(256), 0, s, G, n, D);
+  int rc = launch_status("krum_dist_kernel");
+  if (rc) return rc;
+  if (n > 1) {
+    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), 0, s, D, n, S, J);
+    rc = launch_status("krum_rowsort_kernel");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(krum_rounds_kernel, dim3(1), dim3(1024), 0, s, S, J, n, f, rounds, order, scores0, nullptr);
+  return launch_status("krum_rounds_kernel");
+}
+
+int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds, int* order, float* scores0,
+                void* ws, size_t ws_bytes, hipStream_t s) {
+  SRA_REQUIRE(n >= 1 && n <= kMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d (got %d)", kMaxClients, n);
+  SRA_REQUIRE(rounds >= 1 && rounds <= n, SRA_ERR_ARG, "rounds must be in [1, N] (got %d)", rounds);
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= krum_workspace_bytes(n, d), SRA_ERR_WORKSPACE,
+              "Krum workspace too small: need %zu bytes", krum_workspace_bytes(n, d));
+  const size_t nn = static_cast<size_t>(n) * n;
+  char* base = static_cast<char*>(ws);
+  double* G = reinterpret_cast<double*>(base + 256);
+  char* rest = reinterpret_cast<char*>(G + nn);
+  char* slab = rest + nn * 4 * 3;
+  int rc = launch_gram(X, n, d, ldx, G, slab, gram_workspace_bytes(n, d), s);
+  if (rc) return rc;
+  return launch_krum_rounds_from_gram(G, n, f, rounds, order, scores0, rest, s);
+}
+
+}  // namespace sra
+
+using namespace sra;
+
+extern "C" int sra_krum_workspace_bytes(int64_t n, int64_t d, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && n <= kMaxClients && d >= 1, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kMaxClients);
+  *bytes = krum_workspace_bytes(static_cast<int>(n), d);
+  return SRA_OK;
+}
+
+extern "C" int sra_krum_select_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t rounds,
+                                   int32_t* order, float* scores, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && order != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad d/ldx (%lld/%lld)", (long long)d, (long long)ldx);
+  return launch_krum(X, static_cast<int>(n), d, ldx, f, rounds, order, scores, ws, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t rounds, int32_t* order,
+                                  float* scores, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(G != nullptr && order != nullptr && ws != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= kMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kMaxClients);
+  SRA_REQUIRE(rounds >= 1 && rounds <= n, SRA_ERR_ARG, "rounds must be in [1, N]");
+  SRA_REQUIRE(ws_bytes >= static_cast<size_t>(n) * n * 12, SRA_ERR_WORKSPACE, "workspace too small");
+  return launch_krum_rounds_from_gram(G, static_cast<int>(n), f, rounds, order, scores, static_cast<char*>(ws),
+                                      static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_gather_rows_f32(const float* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows,
+                                   float* out, int64_t ldo, void* stream) {
+  SRA_REQUIRE(X != nullptr && rows != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(nrows >= 1 && d >= 1 && ldo >= d && ldx >= d, SRA_ERR_SHAPE, "bad gather shape");
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(d, 256), nrows), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     X, d, ldx, rows, nrows, out, ldo);
+  return launch_status("gather_rows_kernel");
+}

@@ -71,3 +71,83 @@ def trimmed_mean(X, beta=0.1, out=None):
     _lib.call("sra_trimmed_mean_f32", X.data_ptr(), n, d, ldx, trim_count(n, beta), out.data_ptr(),
               _stream_ptr(X.device))
     return out
+
+
+# ---------------------------------------------------------------------------
+# pairwise L2 / Krum family
+# ---------------------------------------------------------------------------
+def _workspace(nbytes, device):
+    """Caller-owned workspace (torch's caching allocator: no hipMalloc per call)."""
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def gram(X):
+    """Centred Gram (N x N float64) of the client rows (k2, MFMA)."""
+    X, n, d, ldx = as_matrix(X)
+    G = torch.empty((n, n), dtype=torch.float64, device=X.device)
+    nb = _lib.query_bytes("sra_gram_workspace_bytes", n, d)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_gram_f32", X.data_ptr(), n, d, ldx, G.data_ptr(), ws.data_ptr(), nb, _stream_ptr(X.device))
+    return G
+
+
+def krum_select(X, f, rounds=1, scores=True):
+    """Run `rounds` Krum selections (f fixed) on device.
+
+    Returns (order int32 tensor of length `rounds`, scores float32 tensor of
+    the N round-0 scores or None).  No host synchronisation."""
+    X, n, d, ldx = as_matrix(X)
+    order = torch.empty(rounds, dtype=torch.int32, device=X.device)
+    sc = torch.empty(n, dtype=torch.float32, device=X.device) if scores else None
+    nb = _lib.query_bytes("sra_krum_workspace_bytes", n, d)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_krum_select_f32", X.data_ptr(), n, d, ldx, int(f), int(rounds), order.data_ptr(),
+              sc.data_ptr() if sc is not None else None, ws.data_ptr(), nb, _stream_ptr(X.device))
+    return order, sc
+
+
+def krum_from_gram(G, f, rounds=1, scores=True):
+    """Krum selections from a precomputed (e.g. all-reduced) Gram."""
+    n = int(G.shape[0])
+    order = torch.empty(rounds, dtype=torch.int32, device=G.device)
+    sc = torch.empty(n, dtype=torch.float32, device=G.device) if scores else None
+    ws = _workspace(12 * n * n, G.device)
+    _lib.call("sra_krum_from_gram", G.contiguous().data_ptr(), n, int(f), int(rounds), order.data_ptr(),
+              sc.data_ptr() if sc is not None else None, ws.data_ptr(), 12 * n * n, _stream_ptr(G.device))
+    return order, sc
+
+
+def gather_rows(X, rows, out=None):
+    """out[r] = X[rows[r]] with `rows` a device int32 tensor (no host sync)."""
+    X, n, d, ldx = as_matrix(X)
+    k = int(rows.numel())
+    if out is None:
+        out = torch.empty((k, d), dtype=torch.float32, device=X.device)
+    _lib.call("sra_gather_rows_f32", X.data_ptr(), d, ldx, rows.data_ptr(), k, out.data_ptr(), out.stride(0),
+              _stream_ptr(X.device))
+    return out
+
+
+def krum(X, f):
+    """Device Krum: (chosen row as a device copy (d,), order int32 tensor (1,))."""
+    order, _ = krum_select(X, f, 1, scores=False)
+    return gather_rows(X, order)[0], order
+
+
+def bucket_means(X, bucket_size, nbuckets, out=None):
+    """Means of consecutive buckets of clients (np.mean order), (B, d)."""
+    X, n, d, ldx = as_matrix(X)
+    if out is None:
+        out = torch.empty((nbuckets, d), dtype=torch.float32, device=X.device)
+    _lib.call("sra_bucket_mean_f32", X.data_ptr(), n, d, ldx, int(bucket_size), int(nbuckets), out.data_ptr(),
+              out.stride(0), _stream_ptr(X.device))
+    return out
+
+
+def mom_krum(X, f, bucket_size=3):
+    """robust_estimator.mom_krum on device: Krum over ceil(N/3) bucket means."""
+    n = int(X.shape[0])
+    nb = -(-n // bucket_size)
+    B = bucket_means(X, bucket_size, nb)
+    row, order = krum(B, f)
+    return row, order

@@ -105,3 +105,31 @@ def average(samples):
     """The inline ``--agg average`` of simulate.py:235-244 (np.average(axis=0))."""
     st = _stage(samples)
     return st.result(engine.average(st.X))
+
+
+# ---------------------------------------------------------------------------
+# Krum family
+# ---------------------------------------------------------------------------
+def krum_(samples, f):
+    """robust_estimator.py:234-244: the list of per-client Krum scores."""
+    st = _stage(samples)
+    _, scores = engine.krum_select(st.X, f, 1, scores=True)
+    if st.device_io:
+        return scores
+    return [np.float32(v) for v in scores.cpu().numpy()]
+
+
+def krum(samples, f):
+    """robust_estimator.py:246-249: (the chosen sample itself, its index).
+    Like the reference, the returned array IS the caller's object."""
+    st = _stage(samples)
+    order, _ = engine.krum_select(st.X, f, 1, scores=False)
+    idx = int(order.cpu()[0])
+    return samples[idx], idx
+
+
+def mom_krum(samples, f, bucket_size=3):
+    """robust_estimator.py:251-257 (``--agg clustering``)."""
+    st = _stage(samples)
+    row, _ = engine.mom_krum(st.X, f, bucket_size)
+    return st.result(row)
