@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--agg", default="trimmedmean", choices=["trimmedmean", "median", "average"])
+    ap.add_argument("--agg", default="trimmedmean", choices=["trimmedmean", "median", "average", "krum", "mom_krum"])
     ap.add_argument("--clients", type=int, default=128)
     ap.add_argument("--d", type=float, default=1e8, help="coordinates per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -59,23 +59,39 @@ def parse():
     return ap.parse_args()
 
 
+def _krum_step(X, out):
+    row, order = engine.krum(X, 20)
+    out.copy_(row)
+
+
+def _mom_krum_step(X, out):
+    row, order = engine.mom_krum(X, 20)
+    out.copy_(row)
+
+
 AGG = {
     "trimmedmean": lambda X, out: engine.trimmed_mean(X, 0.1, out=out),
     "median": lambda X, out: engine.median(X, out=out),
     "average": lambda X, out: engine.average(X, out=out),
+    "krum": _krum_step,
+    "mom_krum": _mom_krum_step,
 }
 KERNEL_NAME = {
-    "trimmedmean": "select_reg_kernel<128, 1>",
-    "median": "select_reg_kernel<128, 0>",
+    "trimmedmean": "select_reg_kernel<128, 1, 128, 12>",
+    "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
+    "krum": "whole krum op (gram_partial_kernel<4> dominant; per-kernel split in profiles/)",
+    "mom_krum": "whole mom_krum op (bucket means + Gram + scoring)",
 }
+MFMA_PEAK_TFLOPS = 157.3  # fp32 MFMA (MI355X_MICROARCH.md)
 
 
 def cpu_baseline(agg, n, budget_s):
     """Time the oracle's CPU port on N x 1e6 chunks until ~budget_s elapsed."""
     from oracle import robust_np as orc
-    fn = {"trimmedmean": orc.trimmed_mean, "median": orc.median, "average": orc.average}[agg]
-    d = 1_000_000
+    fn = {"trimmedmean": orc.trimmed_mean, "median": orc.median, "average": orc.average,
+          "krum": lambda xs: orc.krum(xs, 20), "mom_krum": lambda xs: orc.mom_krum(xs, 20)}[agg]
+    d = 1_000_000 if agg not in ("krum", "mom_krum") else 100_000
     rng = np.random.default_rng(0)
     x = (0.01 * rng.standard_normal((n, d))).astype(np.float32)
     samples = list(x)
@@ -172,6 +188,12 @@ def main():
 
     alg_bytes = 4 * n * d + 4 * d
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
+    if a.agg in ("krum", "mom_krum"):
+        m = n if a.agg == "krum" else -(-n // 3)
+        flops = m * (m + 1) * d            # upper-triangle centred Gram, 2 flops per FMA
+        bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS, "TFLOP/s"
+        achieved = flops / (kern_ms * 1e-3) / 1e12
     traffic = None
     try:
         with open(a.traffic_json) as fh:
@@ -198,8 +220,8 @@ def main():
                        a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
                    "parallelism": "d-shard x%d" % world},
-        "roofline": {"bound": "hbm", "kernel": KERNEL_NAME[a.agg], "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "roofline": {"bound": bound, "kernel": KERNEL_NAME[a.agg], "achieved": round(achieved, 2),
+                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic, "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
     }

@@ -120,6 +120,24 @@ int sra_gather_rows_f32(const float* X, int64_t d, int64_t ldx, const int32_t* r
 int sra_bucket_mean_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size, int32_t nbuckets,
                         float* out, int64_t ldo, void* stream);
 
+
+/* ------------------------------------------------------------------------ */
+/* Bulyan (k4)                                                               */
+/* ------------------------------------------------------------------------ */
+
+/* Workspace for sra_bulyan_f32, in bytes (mode: 0 krum, 1 median, 2 trimmedmean). */
+int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32_t mode, size_t* bytes);
+
+/* robust_estimator.bulyan (src/robust_estimator.py:277-332): theta = n - 2f
+ * selection rounds (mode 0: Krum with f fixed, the chosen clients; 1/2: the
+ * coordinate-wise median / trimmed mean (beta 0.1) of the remaining clients,
+ * whose nearest client is removed), then the per-coordinate Bulyan median
+ * with numpy's fp64 pairwise tie-break and the mean of the beta = theta - 2f
+ * nearest values.  out: d float64 values.  selected (optional, theta int32):
+ * the chosen clients in krum mode.  theta <= 0 -> SRA_ERR_THETA. */
+int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
+                   int32_t* selected, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

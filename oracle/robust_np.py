@@ -194,6 +194,78 @@ def bulyan_coordinates(selected, beta, block=2048):
     return out
 
 
+def _pw64(a):
+    """numpy's pairwise float64 summation order, restated (loops_utils.h.src)."""
+    n = len(a)
+    if n < 8:
+        r = 0.0
+        for v in a:
+            r += v
+        return r
+    if n <= 128:
+        acc = [a[k] for k in range(8)]
+        i = 8
+        while i < n - (n % 8):
+            for k in range(8):
+                acc[k] += a[i + k]
+            i += 8
+        res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]))
+        while i < n:
+            res += a[i]
+            i += 1
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return _pw64(a[:n2]) + _pw64(a[n2:])
+
+
+def bulyan_one_coordinate_leftfirst(arr, beta):
+    """bulyan_one_coordinate with a DEFINED tie rule for the beta-nearest set.
+
+    The reference takes np.argsort(distances)[:beta]; numpy's quicksort is
+    unstable, so when a value left of the Bulyan median and one right of it are
+    at exactly the same distance, which one enters the set depends on the numpy
+    build (introsort in 1.21, x86-simd-sort AVX-512 in 2.x).  This restatement
+    (and the GPU kernel) grows the window left-first on such ties; everywhere
+    else it equals the reference bit for bit."""
+    a = np.asarray(arr, dtype=np.float64)
+    theta = len(a)
+    m, _ = bulyan_median(a)
+    am = a[m]
+    v = np.sort(a)
+    pl = int(np.searchsorted(v, am, side="left"))
+    pr = int(np.searchsorted(v, am, side="right")) - 1
+    seq = [am] * min(pr - pl + 1, beta)
+    l, r = pl, pr
+    while len(seq) < beta:
+        dl = am - v[l - 1] if l > 0 else np.inf
+        dr = v[r + 1] - am if r < theta - 1 else np.inf
+        if dl <= dr:
+            l -= 1
+            seq.append(v[l])
+        else:
+            r += 1
+            seq.append(v[r])
+    if beta <= 0:
+        return np.nan
+    return _pw64(seq) / beta
+
+
+def bulyan_boundary_tie(arr, beta):
+    """True when the beta-nearest set of a coordinate is ambiguous: values on
+    both sides of the Bulyan median at exactly the boundary distance."""
+    a = np.asarray(arr, dtype=np.float64)
+    m, row = bulyan_median(a)
+    if beta <= 0 or beta >= len(a):
+        return False
+    dist = np.sort(row)
+    cut = dist[beta - 1]
+    if dist[beta] != cut:
+        return False
+    at = a[row == cut]
+    return bool((at < a[m]).any() and (at > a[m]).any())
+
+
 def bulyan_select(rows, f, aggsubfunc):
     """The theta selection rounds of robust_estimator.py:286-322.
 

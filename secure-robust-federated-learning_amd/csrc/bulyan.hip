@@ -1,0 +1,448 @@
+// k4 — Bulyan (src/robust_estimator.py:259-332).
+//
+// Selection (theta = N - 2f rounds, :286-322):
+//   krum        -> k3 krum rounds on the k2 Gram (krum.hip), the chosen clients
+//                  themselves are the selected vectors;
+//   median /    -> per round: k-select over the remaining clients (row list) ->
+//   trimmedmean    aggregate vector (row t of S); squared distance of every
+//                  remaining client to it; the first strict minimum is removed
+//                  from the (order-preserving) device row list.  No host sync
+//                  between rounds.
+// Per-coordinate stage (:324-330, bulyan_one_coordinate/bulyan_median), one
+// lane per coordinate, beta = theta - 2f:
+//   1. sort the theta selected values (register network);
+//   2. the Bulyan median m = argmin_i sum_j |a_i - a_j| (first index) is a
+//      middle order statistic; for even theta the lower and upper middles tie
+//      in exact arithmetic and numpy's fp64 pairwise row sum (8 accumulators,
+//      in selection order) decides -- emulated exactly here;
+//   3. the beta values nearest a_m (np.argsort of the distance row) form a
+//      contiguous window of the sorted values, grown left on <= ties;
+//   4. their mean, summed in that (distance) order with numpy's pairwise
+//      scheme in fp64, is the output (float64, like the reference).
+#include "sra_common.hpp"
+
+namespace sra {
+
+int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds, int* order, float* scores0,
+                void* ws, size_t ws_bytes, hipStream_t s);
+size_t krum_workspace_bytes(int n, int64_t d);
+
+enum BulyanMode { kBulyanKrum = 0, kBulyanMedian = 1, kBulyanTrimmed = 2 };
+constexpr int kMaxClientsBulyan = 256;
+
+// ---------------------------------------------------------------------------
+// k-select over a device row list (median / trimmed mean of the remaining set)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ const char* uniform_ptr(const char* p) {
+  const uint64_t r = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(r >> 32));
+  return reinterpret_cast<const char*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ float ld_lane(const char* row, unsigned off) {
+  typedef const __attribute__((address_space(1))) float gfloat;
+  return __builtin_nontemporal_load(reinterpret_cast<gfloat*>(reinterpret_cast<uint64_t>(row) + off));
+}
+
+template <int P, int MODE>  // MODE: 0 median, 1 trimmed; n in (P-16, P] (P=16: 1..16)
+__global__ void __launch_bounds__(256) select_rows_kernel(const float* __restrict__ X, int64_t ldx,
+                                                          const int* __restrict__ rows, int n, int64_t d, int lo,
+                                                          int hi, float* __restrict__ out) {
+  constexpr int P2 = next_pow2(P);
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256;
+  const int64_t rem = d - base;
+  const unsigned t = threadIdx.x;
+  const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
+  const unsigned off = (t < last ? t : last) * 4u;
+  const int k_bottom = MODE == 0 ? (P - n) / 2 : 0;
+  float v[P2];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int r = i < n ? i : n - 1;
+    const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(rows[r]) * ldx + base));
+    const float x = ld_lane(rp, off);
+    __builtin_amdgcn_sched_barrier(0);
+    const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
+    v[i] = i < n ? x : pad;
+  }
+  float m = v[0];
+#pragma unroll
+  for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, (i < n) ? v[i] : v[0]);
+  int nan_cnt = 0;
+  if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const bool isn = __builtin_isnan(v[i]);
+      nan_cnt += isn ? 1 : 0;
+      v[i] = isn ? __builtin_inff() : v[i];
+    }
+  }
+  float res;
+  if constexpr (MODE == 0) {
+    network_fast<P2, P, P / 2 - 1, P / 2 + 1>(v);
+    res = (n & 1) ? v[P / 2 - 1] : (v[P / 2 - 1] + v[P / 2]) * 0.5f;
+    if (nan_cnt > 0) res = qnan();
+  } else {
+    network_fast<P2, P, 0, P>(v);
+    float acc = 0.f;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if (p >= lo && p < hi) {
+        asm volatile("");
+        acc += v[p];
+      }
+    }
+    res = acc / static_cast<float>(hi - lo);
+    if (nan_cnt > n - hi) res = qnan();
+  }
+  if (t < rem) out[base + t] = res;
+}
+
+// ---------------------------------------------------------------------------
+// squared L2 distance of every listed row to `agg`: partial sums per
+// (row position, coordinate chunk), fp32 within a chunk, reduced in fp64 in a
+// fixed order by bulyan_pick_kernel.
+// ---------------------------------------------------------------------------
+constexpr int kDistChunks = 128;
+
+__global__ void __launch_bounds__(256) row_dist_partial_kernel(const float* __restrict__ X, int64_t ldx,
+                                                               const int* __restrict__ rows, int64_t d,
+                                                               const float* __restrict__ agg, int64_t chunk,
+                                                               float* __restrict__ partial) {
+  const int c = blockIdx.x;      // coordinate chunk
+  const int rp = blockIdx.y;     // position in the row list
+  const float* x = X + static_cast<int64_t>(rows[rp]) * ldx;
+  const int64_t j0 = static_cast<int64_t>(c) * chunk;
+  const int64_t j1 = j0 + chunk < d ? j0 + chunk : d;
+  float s = 0.f;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+    const float df = agg[j] - x[j];
+    s = __builtin_fmaf(df, df, s);
+  }
+  // block reduce (fixed order)
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[static_cast<int64_t>(rp) * kDistChunks + c] = red[0];
+}
+
+// argmin (first strict minimum, NaN never chosen) of the listed rows'
+// distances; removes it from the list (order preserved) into rows_next.
+__global__ void __launch_bounds__(256) bulyan_pick_kernel(const float* __restrict__ partial, const int* __restrict__ rows,
+                                                         int nr, int nchunks, int* __restrict__ rows_next,
+                                                         int* __restrict__ status) {
+  __shared__ double dist[kMaxClientsBulyan];
+  __shared__ int pick;
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+    double s = 0.0;
+    for (int c = 0; c < nchunks; ++c) s += static_cast<double>(partial[static_cast<int64_t>(r) * kDistChunks + c]);
+    dist[r] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = -1;
+    double bv = __builtin_inf();
+    for (int r = 0; r < nr; ++r) {
+      // the reference compares fp32 norms: sqrt is monotone, compare squares
+      if (dist[r] < bv) { bv = dist[r]; best = r; }
+    }
+    pick = best;
+    if (best < 0) *status = 1;  // AssertionError in the reference (all NaN)
+  }
+  __syncthreads();
+  const int p = pick < 0 ? 0 : pick;
+  for (int r = threadIdx.x; r < nr - 1; r += blockDim.x) rows_next[r] = rows[r < p ? r : r + 1];
+}
+
+// ---------------------------------------------------------------------------
+// per-coordinate Bulyan stage
+// ---------------------------------------------------------------------------
+// numpy pairwise fp64 sum of f(0..n) for n <= 128 (eight accumulators)
+template <typename F>
+__device__ __forceinline__ double np_pw_block64(int n, F&& f) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; ++i) res += f(i);
+    return res;
+  }
+  double r0 = f(0), r1 = f(1), r2 = f(2), r3 = f(3), r4 = f(4), r5 = f(5), r6 = f(6), r7 = f(7);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += f(i); r1 += f(i + 1); r2 += f(i + 2); r3 += f(i + 3);
+    r4 += f(i + 4); r5 += f(i + 5); r6 += f(i + 6); r7 += f(i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += f(i);
+  return res;
+}
+
+template <typename F>
+__device__ __forceinline__ double np_pw64(int lo, int n, F&& f) {
+  if (n <= 128) return np_pw_block64(n, [&](int i) { return f(lo + i); });
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  auto half = [&](int l2, int m2) -> double {
+    if (m2 <= 128) return np_pw_block64(m2, [&](int i) { return f(l2 + i); });
+    int q = m2 / 2;
+    q -= q % 8;
+    return np_pw_block64(q, [&](int i) { return f(l2 + i); }) +
+           np_pw_block64(m2 - q, [&](int i) { return f(l2 + q + i); });
+  };
+  return half(lo, n2) + half(lo + n2, n - n2);
+}
+
+template <int P>  // theta <= P; 64-thread blocks (one wave), sorted columns in LDS
+__global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
+                                                          const int* __restrict__ rows, int theta, int beta,
+                                                          int64_t d, double* __restrict__ out) {
+  constexpr int P2 = next_pow2(P);
+  __shared__ float col[P][64];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t rem = d - base;
+  const int t = threadIdx.x;
+  const int tl = t < rem ? t : static_cast<int>(rem - 1);
+  const int64_t j = base + tl;
+  auto a_orig = [&](int i) -> float { return S[static_cast<int64_t>(rows[i]) * lds_ + j]; };
+
+  float v[P2];
+  bool has_nan = false;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const float x = i < theta ? a_orig(i) : __builtin_inff();
+    has_nan |= __builtin_isnan(x);
+    v[i] = x;
+  }
+  if (__builtin_amdgcn_ballot_w64(has_nan) != 0) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
+  }
+  network_fast<P2, P, 0, P>(v);
+#pragma unroll
+  for (int i = 0; i < P; ++i) col[i][t] = v[i];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+
+  // 1. Bulyan median: middle order statistic(s), fp64 pairwise tie-break
+  double am;
+  if (theta & 1) {
+    am = col[(theta - 1) / 2][t];
+  } else {
+    const float L = col[theta / 2 - 1][t];
+    const float U = col[theta / 2][t];
+    if (L == U) {
+      am = L;
+    } else {
+      const double TL = np_pw64(0, theta, [&](int i) { return __builtin_fabs(static_cast<double>(L) - a_orig(i)); });
+      const double TU = np_pw64(0, theta, [&](int i) { return __builtin_fabs(static_cast<double>(U) - a_orig(i)); });
+      if (TL < TU) {
+        am = L;
+      } else if (TU < TL) {
+        am = U;
+      } else {
+        int fL = theta, fU = theta;
+        for (int i = theta - 1; i >= 0; --i) {
+          const float a = a_orig(i);
+          if (a == L) fL = i;
+          if (a == U) fU = i;
+        }
+        am = fL < fU ? L : U;
+      }
+    }
+  }
+  // 2. run of values equal to a_m in the sorted column
+  int pl = (theta - 1) / 2, pr;
+  while (pl > 0 && static_cast<double>(col[pl][t]) > am) --pl;
+  while (pl < theta - 1 && static_cast<double>(col[pl][t]) < am) ++pl;
+  while (pl > 0 && static_cast<double>(col[pl - 1][t]) == am) --pl;
+  pr = pl;
+  while (pr + 1 < theta && static_cast<double>(col[pr + 1][t]) == am) ++pr;
+
+  // 3. beta nearest, in argsort (distance) order; 4. numpy pairwise fp64 mean
+  int l = pl, r = pr, taken = 0;
+  auto next = [&]() -> double {
+    // run elements first (distance 0), then grow left on <= ties
+    if (taken < pr - pl + 1) {
+      ++taken;
+      return am;
+    }
+    const double dl = l > 0 ? am - static_cast<double>(col[l - 1][t]) : __builtin_inf();
+    const double dr = r < theta - 1 ? static_cast<double>(col[r + 1][t]) - am : __builtin_inf();
+    ++taken;
+    if (dl <= dr) {
+      --l;
+      return static_cast<double>(col[l][t]);
+    }
+    ++r;
+    return static_cast<double>(col[r][t]);
+  };
+  double res;
+  if (beta <= 0) {
+    res = __builtin_nan("");  // mean of an empty slice (beta = 0) / dropped tail
+  } else if (beta < 8) {
+    res = 0.0;
+    for (int i = 0; i < beta; ++i) res += next();
+  } else {
+    // eight accumulators over the first beta - beta%8 values, then the tail
+    // (beta <= 128; a larger beta uses the same order with one accumulator
+    // set, within fp64 rounding of numpy's recursive split)
+    double r0 = next(), r1 = next(), r2 = next(), r3 = next(), r4 = next(), r5 = next(), r6 = next(), r7 = next();
+    int i = 8;
+    for (; i < beta - (beta % 8); i += 8) {
+      r0 += next(); r1 += next(); r2 += next(); r3 += next();
+      r4 += next(); r5 += next(); r6 += next(); r7 += next();
+    }
+    res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < beta; ++i) res += next();
+  }
+  res = res / static_cast<double>(beta);
+  if (has_nan) res = __builtin_nan("");
+  if (t < rem) out[base + t] = res;
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+struct BulyanWs {
+  char* krum_ws;      // krum mode
+  size_t krum_bytes;
+  int* order;         // theta selected client indices (krum) / identity rows (S)
+  int* rows_a;        // row lists (ping-pong)
+  int* rows_b;
+  int* status;
+  float* S;           // theta x d aggregates (median / trimmed modes)
+  float* partial;     // N x kDistChunks
+};
+
+size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
+  const int theta = n - 2 * f;
+  size_t b = 4096 + 4 * static_cast<size_t>(n) * 4 + 256;
+  if (mode == kBulyanKrum) {
+    b += krum_workspace_bytes(n, d);
+  } else {
+    b += sizeof(float) * static_cast<size_t>(theta > 0 ? theta : 0) * static_cast<size_t>(d) + 256;
+    b += sizeof(float) * static_cast<size_t>(n) * kDistChunks;
+  }
+  return b;
+}
+
+template <int MODE>
+static int launch_select_rows(const float* X, int64_t ldx, const int* rows, int n, int64_t d, int lo, int hi,
+                              float* out, hipStream_t s) {
+  const int64_t blocks = cdiv(d, 256);
+  const int P = static_cast<int>(cdiv(n, 16) * 16);
+#define SRA_SR(PP)                                                                                               \
+  case PP:                                                                                                       \
+    hipLaunchKernelGGL((select_rows_kernel<PP, MODE>), dim3(blocks), dim3(256), 0, s, X, ldx, rows, n, d, lo, hi, \
+                       out);                                                                                     \
+    return launch_status("select_rows_kernel");
+  switch (P) {
+    SRA_SR(16) SRA_SR(32) SRA_SR(48) SRA_SR(64) SRA_SR(80) SRA_SR(96) SRA_SR(112) SRA_SR(128)
+    default: break;
+  }
+#undef SRA_SR
+  set_error("bulyan median/trimmedmean rounds support N <= 128 (got %d)", n);
+  return SRA_ERR_UNSUPPORTED;
+}
+
+static int launch_final(const float* S, int64_t lds_, const int* rows, int theta, int beta, int64_t d, double* out,
+                        hipStream_t s) {
+  const int64_t blocks = cdiv(d, 64);
+  const int P = static_cast<int>(cdiv(theta, 16) * 16);
+#define SRA_FIN(PP)                                                                                              \
+  case PP:                                                                                                       \
+    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(blocks), dim3(64), 0, s, S, lds_, rows, theta, beta, d, out); \
+    return launch_status("bulyan_final_kernel");
+  switch (P) {
+    SRA_FIN(16) SRA_FIN(32) SRA_FIN(48) SRA_FIN(64) SRA_FIN(80) SRA_FIN(96) SRA_FIN(112) SRA_FIN(128)
+    default: break;
+  }
+#undef SRA_FIN
+  set_error("bulyan per-coordinate stage supports theta <= 128 (got %d)", theta);
+  return SRA_ERR_UNSUPPORTED;
+}
+
+__global__ void iota_kernel(int* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = i;
+}
+
+int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode, double* out, int* sel_out,
+                  void* ws, size_t ws_bytes, hipStream_t s) {
+  const int theta = n - 2 * f;
+  SRA_REQUIRE(theta > 0, SRA_ERR_THETA, "bulyan needs theta = N - 2f > 0 (N=%d, f=%d)", n, f);
+  SRA_REQUIRE(mode >= 0 && mode <= 2, SRA_ERR_ARG, "bad bulyan mode %d", mode);
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= bulyan_workspace_bytes(n, d, mode, f), SRA_ERR_WORKSPACE,
+              "bulyan workspace too small: need %zu bytes", bulyan_workspace_bytes(n, d, mode, f));
+  const int beta = theta - 2 * f;
+  char* p = static_cast<char*>(ws);
+  int* order = reinterpret_cast<int*>(p + 256);
+  int* rows_a = order + n;
+  int* rows_b = rows_a + n;
+  int* status = rows_b + n;
+  char* rest = p + 4096 + 4 * static_cast<size_t>(n) * 4;
+  int rc;
+  if (mode == kBulyanKrum) {
+    rc = launch_krum(X, n, d, ldx, f, theta, order, nullptr, rest, krum_workspace_bytes(n, d), s);
+    if (rc) return rc;
+    if (sel_out) SRA_HIP(hipMemcpyAsync(sel_out, order, sizeof(int) * theta, hipMemcpyDeviceToDevice, s));
+    return launch_final(X, ldx, order, theta, beta, d, out, s);
+  }
+  SRA_REQUIRE(n <= 128, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= 128 (got %d)", n);
+  float* S = reinterpret_cast<float*>(rest);
+  float* partial = S + static_cast<size_t>(theta) * static_cast<size_t>(d) + 64;
+  hipLaunchKernelGGL(iota_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, rows_a, n);
+  hipLaunchKernelGGL(iota_kernel, dim3(cdiv(theta, 256)), dim3(256), 0, s, order, theta);
+  rc = launch_status("iota_kernel");
+  if (rc) return rc;
+  const int64_t chunk = cdiv(d, kDistChunks);
+  const int nchunks = static_cast<int>(cdiv(d, chunk));
+  int* cur = rows_a;
+  int* nxt = rows_b;
+  for (int t = 0; t < theta; ++t) {
+    const int nr = n - t;
+    float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
+    if (mode == kBulyanMedian) {
+      rc = launch_select_rows<0>(X, ldx, cur, nr, d, 0, nr, agg, s);
+    } else {
+      const int b = static_cast<int>(nr * 0.1);  // trimmed_mean(beta=0.1): int(size * beta)
+      const int lo = b, hi = nr - b > b ? nr - b : b;
+      rc = launch_select_rows<1>(X, ldx, cur, nr, d, lo, hi, agg, s);
+    }
+    if (rc) return rc;
+    hipLaunchKernelGGL(row_dist_partial_kernel, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg, chunk,
+                       partial);
+    rc = launch_status("row_dist_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, partial, cur, nr, nchunks, nxt, status);
+    rc = launch_status("bulyan_pick_kernel");
+    if (rc) return rc;
+    int* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  return launch_final(S, d, order, theta, beta, d, out, s);
+}
+
+}  // namespace sra
+
+using namespace sra;
+
+extern "C" int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32_t mode, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && d >= 1, SRA_ERR_SHAPE, "bad shape");
+  *bytes = bulyan_workspace_bytes(static_cast<int>(n), d, mode, f);
+  return SRA_OK;
+}
+
+extern "C" int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode,
+                              double* out, int32_t* selected, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= 256 && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= 256)");
+  return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
+                       static_cast<hipStream_t>(stream));
+}

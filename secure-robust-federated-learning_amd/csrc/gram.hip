@@ -30,21 +30,30 @@
 // bound (~1.05 ms per 1e7 coordinates at the 157 TF fp32 MFMA peak).
 #include "sra_common.hpp"
 
+#include <cstdlib>
+
 namespace sra {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kStage = 64;            // coordinates per stage
-constexpr int kRowPad = kStage + 4;   // LDS row stride in floats
-
-template <int NB>
+template <int NB, int WAVES = 4>
 struct GramCfg {
   static constexpr int NP = 32 * NB;
-  static constexpr int T = NB * (NB + 1) / 2;                  // upper-triangle tiles
-  static constexpr int WT = NB <= 4 ? 1 : (NB <= 6 ? 2 : 4);   // tile groups
-  static constexpr int WK = 4 / WT;                            // k groups
-  static constexpr int TPW = (T + WT - 1) / WT;                // tiles per wave (max)
-  static constexpr int LOADS = NP * (kStage / 4) / 256;        // float4 per thread per stage
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int STAGE = NB <= 4 ? 128 : 64;                // coordinates per stage
+  static constexpr int ROWPAD = STAGE + 4;                       // LDS row stride (floats)
+  static constexpr int T = NB * (NB + 1) / 2;                    // upper-triangle tiles
+  // tile groups: 4 waves -> keep <= 176 accumulators per wave; 8 waves (two
+  // per SIMD) -> <= 128 so that a wave fits in 256 registers
+  static constexpr int WT = WAVES == 4 ? (NB <= 4 ? 1 : (NB <= 6 ? 2 : 4))
+                                       : (NB <= 3 ? 1 : (NB <= 5 ? 2 : (NB <= 7 ? 4 : 8)));
+  static constexpr int WK = WAVES / WT;                          // k groups
+  static constexpr int TPW = (T + WT - 1) / WT;                  // tiles per wave (max)
+  static constexpr int GROUPS = STAGE / 8;                       // 8-coordinate groups per stage
+  static constexpr int GPW = GROUPS / WK;                        // groups per wave per stage
+  static constexpr int C4 = STAGE / 4;                           // float4 columns per row
+  static constexpr int RSTEP = THREADS / C4;                     // rows covered per load sweep
+  static constexpr int LOADS = NP / RSTEP > 0 ? NP / RSTEP : 1;  // float4 per thread per stage
   static constexpr int kTileI(int t) {
     int c = 0;
     for (int i = 0; i < NB; ++i)
@@ -63,24 +72,37 @@ struct GramCfg {
       }
     return 0;
   }
-  static constexpr int lds_floats = 2 * NP * kRowPad + 2 * kStage + 16 * kStage;
+  static constexpr int BUF = NP * ROWPAD;                        // floats per stage buffer
+  static constexpr int PART = WAVES * STAGE;                     // per-wave column partials
+  static constexpr int lds_floats = 2 * BUF + 2 * PART;
 };
 
-int gram_slab_floats(int nb, int64_t num_wg) {
-  const int T = nb * (nb + 1) / 2;
-  const int WT = nb <= 4 ? 1 : (nb <= 6 ? 2 : 4);
-  return static_cast<int>(num_wg * (4 / WT) * T * 1024);
+template <int NB, int WAVES>
+int gram_slab_floats_t(int64_t num_wg) {
+  using C = GramCfg<NB, WAVES>;
+  return static_cast<int>(num_wg * C::WK * C::T * 1024);
 }
 
-template <int NB, bool VEC, int TG>
+// sum of x over the 4 lanes {l, l^16, l^32, l^48} of a wave
+__device__ __forceinline__ float sum_lanes_16_32(float x) {
+  // xor 16 inside each 32-lane half (ds_swizzle bit mode: and 0x1f, xor 0x10)
+  x += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), 0x401f));
+  // xor 32 across the halves
+  x += __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(((threadIdx.x & 63) ^ 32) << 2,
+                                                              __builtin_bit_cast(int, x)));
+  return x;
+}
+
+template <int NB, int WAVES, bool VEC, int TG>
 __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, int64_t d, int64_t ldx, int64_t chunk,
                                           float* __restrict__ slab, float* lds) {
-  using C = GramCfg<NB>;
-  constexpr int NP = C::NP;
+  using C = GramCfg<NB, WAVES>;
+  constexpr int STAGE = C::STAGE;
   constexpr int tg = TG;
-  float* buf[2] = {lds, lds + NP * kRowPad};
-  float* meanb[2] = {lds + 2 * NP * kRowPad, lds + 2 * NP * kRowPad + kStage};
-  float* part = lds + 2 * NP * kRowPad + 2 * kStage;  // [16][64]
+  // LDS carve-up (pointers derived arithmetically from the __shared__ base so
+  // the compiler keeps them in the LDS address space: ds_read/ds_write)
+  auto bufp = [&](int which) { return lds + which * C::BUF; };
+  auto partp = [&](int which) { return lds + 2 * C::BUF + which * C::PART; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -88,7 +110,7 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
   const int kg = wave / C::WT;
   const int64_t k_begin = static_cast<int64_t>(blockIdx.x) * chunk;
   const int64_t k_end = k_begin + chunk < d ? k_begin + chunk : d;
-  const int nstage = k_begin < k_end ? static_cast<int>(cdiv(k_end - k_begin, kStage)) : 0;
+  const int nstage = k_begin < k_end ? static_cast<int>(cdiv(k_end - k_begin, STAGE)) : 0;
   const float inv_n = 1.0f / static_cast<float>(n);
 
   f32x16 acc[C::TPW];
@@ -97,18 +119,18 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  // staging registers: thread t owns float4 column c4 = t & 15 of rows (t >> 4) + 16 q
+  // staging: thread t owns float4 column c4 = t % C4 of rows t / C4 + RSTEP * q
   f32x4 stg[C::LOADS];
-  const int c4 = tid & 15;
-  const int row0 = tid >> 4;
+  const int c4 = tid % C::C4;
+  const int row0 = tid / C::C4;
 
   auto load_stage = [&](int s) {
-    const int64_t k0 = k_begin + static_cast<int64_t>(s) * kStage + 4 * c4;
+    const int64_t k0 = k_begin + static_cast<int64_t>(s) * STAGE + 4 * c4;
 #pragma unroll
     for (int q = 0; q < C::LOADS; ++q) {
-      const int row = row0 + 16 * q;
+      const int row = row0 + C::RSTEP * q;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (row < n) {
+      if (row < n && row < C::NP) {
         const float* p = X + static_cast<int64_t>(row) * ldx + k0;
         if (VEC && k0 + 3 < k_end) {
           v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
@@ -120,51 +142,58 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
       stg[q] = v;
     }
   };
-  auto store_stage = [&](float* b) {
+  // registers -> LDS stage buffer, plus this wave's column partial sums
+  // (the 64 lanes of a wave cover C4/…: lanes with equal c4 are reduced by
+  // swizzles, then lanes with lane < C4 own the wave's partial of 4 columns)
+  auto store_stage = [&](float* b, float* part) {
     f32x4 colsum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < C::LOADS; ++q) {
-      const int row = row0 + 16 * q;
-      *reinterpret_cast<f32x4*>(b + row * kRowPad + 4 * c4) = stg[q];
+      const int row = row0 + C::RSTEP * q;
+      if (row < C::NP) *reinterpret_cast<f32x4*>(b + row * C::ROWPAD + 4 * c4) = stg[q];
       colsum += stg[q];
     }
-    *reinterpret_cast<f32x4*>(part + row0 * kStage + 4 * c4) = colsum;
-  };
-  // after a barrier: column means of the stage (real rows only) and mean-filled pad rows
-  auto finish_means = [&](float* b, float* mb) {
-    if (tid < kStage) {
-      float s = 0.f;
+    if constexpr (C::C4 == 16) {
 #pragma unroll
-      for (int p = 0; p < 16; ++p) s += part[p * kStage + tid];
-      const float mu = s * inv_n;
-      mb[tid] = mu;
-      for (int r = n; r < NP; ++r) b[r * kRowPad + tid] = mu;  // centred pad rows are exactly 0
+      for (int e = 0; e < 4; ++e) colsum[e] = sum_lanes_16_32(colsum[e]);
+      if (lane < 16) *reinterpret_cast<f32x4*>(part + wave * STAGE + 4 * c4) = colsum;
+    } else {  // C4 == 32: lanes l and l^32 share columns
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        colsum[e] += __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2,
+                                                                            __builtin_bit_cast(int, colsum[e])));
+      if (lane < 32) *reinterpret_cast<f32x4*>(part + wave * STAGE + 4 * c4) = colsum;
     }
   };
 
   if (nstage > 0) {
     load_stage(0);
-    store_stage(buf[0]);
-    __syncthreads();
-    finish_means(buf[0], meanb[0]);
+    store_stage(bufp(0), partp(0));
     if (nstage > 1) load_stage(1);
     __syncthreads();
   }
 
   const int r = lane & 31;
   const int h = lane >> 5;
+  // rows >= n of the last block are zeroed after centring (their staged value is 0)
+  const float last_mask = (32 * (NB - 1) + r) < n ? 1.f : 0.f;
   for (int s = 0; s < nstage; ++s) {
-    const float* b = buf[s & 1];
-    const float* mb = meanb[s & 1];
+    const float* b = bufp(s & 1);
+    const float* part = partp(s & 1);
     // ---- MFMA over this wave's 8-coordinate groups of the stage ----
-#pragma unroll 1
-    for (int g = kg; g < kStage / 8; g += C::WK) {
+#pragma unroll
+    for (int gi = 0; gi < C::GPW; ++gi) {
+      const int g = kg + C::WK * gi;
       const int col = 8 * g + 4 * h;
-      const f32x4 mu = *reinterpret_cast<const f32x4*>(mb + col);
+      f32x4 mu = *reinterpret_cast<const f32x4*>(part + col);
+#pragma unroll
+      for (int w = 1; w < WAVES; ++w) mu += *reinterpret_cast<const f32x4*>(part + w * STAGE + col);
+      mu *= inv_n;
       f32x4 fr[NB];
 #pragma unroll
       for (int blk = 0; blk < NB; ++blk)
-        fr[blk] = *reinterpret_cast<const f32x4*>(b + (32 * blk + r) * kRowPad + col) - mu;
+        fr[blk] = *reinterpret_cast<const f32x4*>(b + (32 * blk + r) * C::ROWPAD + col) - mu;
+      fr[NB - 1] *= last_mask;
 #pragma unroll
       for (int t = 0; t < C::TPW; ++t) {
         const int tile = tg + C::WT * t;     // compile-time: tg is a template parameter
@@ -176,13 +205,11 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
         }
       }
     }
-    // ---- stage s+1 -> LDS (registers were loaded one stage ahead) ----
+    // ---- stage s+1 -> LDS (its registers were loaded one stage ahead) ----
     if (s + 1 < nstage) {
-      store_stage(buf[(s + 1) & 1]);
+      store_stage(bufp((s + 1) & 1), partp((s + 1) & 1));
       if (s + 2 < nstage) load_stage(s + 2);
     }
-    __syncthreads();
-    if (s + 1 < nstage) finish_means(buf[(s + 1) & 1], meanb[(s + 1) & 1]);
     __syncthreads();
   }
 
@@ -202,23 +229,59 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
   }
 }
 
-template <int NB, bool VEC>
-__global__ void __launch_bounds__(256) gram_partial_kernel(const float* __restrict__ X, int n, int64_t d,
-                                                           int64_t ldx, int64_t chunk, float* __restrict__ slab) {
+template <int NB, int WAVES, bool VEC>
+__global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* __restrict__ X, int n, int64_t d,
+                                                                  int64_t ldx, int64_t chunk,
+                                                                  float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tg = (threadIdx.x >> 6) % GramCfg<NB>::WT;  // wave-uniform
-  if (tg == 0) gram_body<NB, VEC, 0>(X, n, d, ldx, chunk, slab, lds);
-  else if (tg == 1) gram_body<NB, VEC, 1>(X, n, d, ldx, chunk, slab, lds);
-  else if (tg == 2) gram_body<NB, VEC, 2>(X, n, d, ldx, chunk, slab, lds);
-  else gram_body<NB, VEC, 3>(X, n, d, ldx, chunk, slab, lds);
+  constexpr int WT = GramCfg<NB, WAVES>::WT;
+  const int tg = (threadIdx.x >> 6) % WT;  // wave-uniform
+  if (tg == 0) gram_body<NB, WAVES, VEC, 0>(X, n, d, ldx, chunk, slab, lds);
+  if constexpr (WT > 1) if (tg == 1) gram_body<NB, WAVES, VEC, 1>(X, n, d, ldx, chunk, slab, lds);
+  if constexpr (WT > 2) {
+    if (tg == 2) gram_body<NB, WAVES, VEC, 2>(X, n, d, ldx, chunk, slab, lds);
+    if (tg == 3) gram_body<NB, WAVES, VEC, 3>(X, n, d, ldx, chunk, slab, lds);
+  }
+  if constexpr (WT > 4) {
+    if (tg == 4) gram_body<NB, WAVES, VEC, 4>(X, n, d, ldx, chunk, slab, lds);
+    if (tg == 5) gram_body<NB, WAVES, VEC, 5>(X, n, d, ldx, chunk, slab, lds);
+    if (tg == 6) gram_body<NB, WAVES, VEC, 6>(X, n, d, ldx, chunk, slab, lds);
+    if (tg == 7) gram_body<NB, WAVES, VEC, 7>(X, n, d, ldx, chunk, slab, lds);
+  }
 }
 
-// Sum the slab in a fixed order (fp64) and write the symmetric N x N Gram.
+// Slab reduction in a fixed order (deterministic), fp64, two levels:
+//  level 1: block (x, g) sums slab entries [g*per, (g+1)*per) of 256 elements;
+//  level 2: sums the kRedGroups partials in order and mirrors to N x N.
+constexpr int kRedGroups = 32;
+
 template <int NB>
-__global__ void __launch_bounds__(256) gram_reduce_kernel(const float* __restrict__ slab, int n, int64_t nslab,
-                                                          double* __restrict__ G) {
+__global__ void __launch_bounds__(256) gram_reduce1_kernel(const float* __restrict__ slab, int64_t nslab,
+                                                           double* __restrict__ partial) {
   using C = GramCfg<NB>;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (tile, element)
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (e >= C::T * 1024) return;
+  const int64_t per = (nslab + kRedGroups - 1) / kRedGroups;
+  const int64_t w0 = g * per;
+  const int64_t w1 = w0 + per < nslab ? w0 + per : nslab;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int64_t w = w0;
+  for (; w + 4 <= w1; w += 4) {
+    s0 += static_cast<double>(slab[(w + 0) * C::T * 1024 + e]);
+    s1 += static_cast<double>(slab[(w + 1) * C::T * 1024 + e]);
+    s2 += static_cast<double>(slab[(w + 2) * C::T * 1024 + e]);
+    s3 += static_cast<double>(slab[(w + 3) * C::T * 1024 + e]);
+  }
+  for (; w < w1; ++w) s0 += static_cast<double>(slab[w * C::T * 1024 + e]);
+  partial[static_cast<int64_t>(g) * C::T * 1024 + e] = (s0 + s1) + (s2 + s3);
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) gram_reduce2_kernel(const double* __restrict__ partial, int n,
+                                                           double* __restrict__ G) {
+  using C = GramCfg<NB>;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= C::T * 1024) return;
   const int tile = e >> 10;
   const int el = e & 1023;
@@ -226,42 +289,66 @@ __global__ void __launch_bounds__(256) gram_reduce_kernel(const float* __restric
   const int j = 32 * C::kTileJ(tile) + (el & 31);
   if (i >= n || j >= n) return;
   double s = 0.0;
-  for (int64_t w = 0; w < nslab; ++w) s += static_cast<double>(slab[w * C::T * 1024 + e]);
+#pragma unroll 8
+  for (int g = 0; g < kRedGroups; ++g) s += partial[static_cast<int64_t>(g) * C::T * 1024 + e];
   G[static_cast<int64_t>(i) * n + j] = s;
   G[static_cast<int64_t>(j) * n + i] = s;
 }
 
 int gram_num_wg(int64_t d) {
-  const int64_t stages = cdiv(d, kStage);
+  const int64_t stages = cdiv(d, 64);
   return static_cast<int>(stages < 256 ? (stages > 0 ? stages : 1) : 256);
+}
+
+static int gram_waves() {
+  static const int w = [] {
+    const char* e = getenv("SRA_GRAM_WAVES");
+    return (e != nullptr && atoi(e) == 4) ? 4 : 8;
+  }();
+  return w;
+}
+
+template <int NB, int WAVES>
+static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s) {
+  using C = GramCfg<NB, WAVES>;
+  const int nwg = gram_num_wg(d);
+  const int64_t chunk = cdiv(cdiv(d, nwg), C::STAGE) * C::STAGE;
+  const size_t lds = sizeof(float) * C::lds_floats;
+  const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  if (vec) {
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true>), dim3(nwg), dim3(C::THREADS), lds, s, X, n, d, ldx,
+                       chunk, slab);
+  } else {
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false>), dim3(nwg), dim3(C::THREADS), lds, s, X, n, d, ldx,
+                       chunk, slab);
+  }
+  int rc = launch_status("gram_partial_kernel");
+  if (rc) return rc;
+  double* partial = reinterpret_cast<double*>(slab + static_cast<size_t>(gram_slab_floats_t<NB, WAVES>(nwg)));
+  hipLaunchKernelGGL((gram_reduce1_kernel<NB>), dim3(cdiv(C::T * 1024, 256), kRedGroups), dim3(256), 0, s, slab,
+                     static_cast<int64_t>(nwg) * C::WK, partial);
+  rc = launch_status("gram_reduce1_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL((gram_reduce2_kernel<NB>), dim3(cdiv(C::T * 1024, 256)), dim3(256), 0, s, partial, n, G);
+  return launch_status("gram_reduce2_kernel");
 }
 
 template <int NB>
 static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s) {
-  using C = GramCfg<NB>;
-  const int nwg = gram_num_wg(d);
-  const int64_t chunk = cdiv(cdiv(d, nwg), kStage) * kStage;
-  const size_t lds = sizeof(float) * C::lds_floats;
-  const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  if (vec) {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, true>), dim3(nwg), dim3(256), lds, s, X, n, d, ldx, chunk, slab);
-  } else {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, false>), dim3(nwg), dim3(256), lds, s, X, n, d, ldx, chunk, slab);
-  }
-  int rc = launch_status("gram_partial_kernel");
-  if (rc) return rc;
-  hipLaunchKernelGGL((gram_reduce_kernel<NB>), dim3(cdiv(C::T * 1024, 256)), dim3(256), 0, s, slab, n,
-                     static_cast<int64_t>(nwg) * C::WK, G);
-  return launch_status("gram_reduce_kernel");
+  if (gram_waves() == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s);
+  return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s);
 }
 
 size_t gram_workspace_bytes(int n, int64_t d) {
+  // sized for the larger of the 4- and 8-wave slab layouts (WK <= 8)
   const int nb = static_cast<int>(cdiv(n, 32));
-  return sizeof(float) * static_cast<size_t>(gram_slab_floats(nb, gram_num_wg(d)));
+  const int T = nb * (nb + 1) / 2;
+  return sizeof(float) * static_cast<size_t>(gram_num_wg(d)) * 8 * T * 1024 +
+         sizeof(double) * static_cast<size_t>(kRedGroups) * T * 1024;
 }
 
 int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes,

@@ -151,3 +151,26 @@ def mom_krum(X, f, bucket_size=3):
     B = bucket_means(X, bucket_size, nb)
     row, order = krum(B, f)
     return row, order
+
+
+# ---------------------------------------------------------------------------
+# Bulyan
+# ---------------------------------------------------------------------------
+BULYAN_MODES = {"krum": 0, "median": 1, "trimmedmean": 2}
+
+
+def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
+    """robust_estimator.bulyan on device: float64 (d,) aggregate.
+    With selected=True also returns the theta chosen clients (krum mode)."""
+    X, n, d, ldx = as_matrix(X)
+    if aggsubfunc not in BULYAN_MODES:
+        raise ValueError("aggsubfunc must be one of %s" % sorted(BULYAN_MODES))
+    mode = BULYAN_MODES[aggsubfunc]
+    theta = n - 2 * int(f)
+    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    sel = torch.empty(max(theta, 1), dtype=torch.int32, device=X.device) if selected else None
+    nb = _lib.query_bytes("sra_bulyan_workspace_bytes", n, d, int(f), mode)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_bulyan_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
+              sel.data_ptr() if sel is not None else None, ws.data_ptr(), nb, _stream_ptr(X.device))
+    return (out, sel) if selected else out

@@ -133,3 +133,12 @@ def mom_krum(samples, f, bucket_size=3):
     st = _stage(samples)
     row, _ = engine.mom_krum(st.X, f, bucket_size)
     return st.result(row)
+
+
+# ---------------------------------------------------------------------------
+# Bulyan
+# ---------------------------------------------------------------------------
+def bulyan(grads, f, aggsubfunc="trimmedmean"):
+    """robust_estimator.py:277-332 (float64 result, like the reference)."""
+    st = _stage(grads)
+    return st.result(engine.bulyan(st.X, f, aggsubfunc), dtype=np.float64)

@@ -1,0 +1,82 @@
+"""GPU parity of Bulyan (k4) in all three selection modes against the golden
+fixtures and the oracle.
+
+The selection (which clients / aggregates enter the per-coordinate stage), the
+Bulyan median pick (numpy's fp64 pairwise tie-break for even theta) and the
+beta-window are discrete decisions reproduced exactly; the final fp64 mean is
+summed in the same (distance) order with numpy's pairwise scheme, so the
+result matches to fp64 rounding (rtol 1e-12)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import fixtures, gpu_available
+from oracle import robust_np as orc
+from synth import make_rows
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from srfl_amd import engine, robust_estimator as gre
+
+BY = fixtures(func="bulyan")
+
+
+def _leftfirst_and_ties(xs, f, mode):
+    """The defined-tie restatement of the per-coordinate stage over the
+    oracle's (bit-exact) selection, plus the coordinates where the reference's
+    own result depends on numpy's unstable argsort."""
+    rows = [np.asarray(r).ravel() for r in xs]
+    sel, _ = orc.bulyan_select(rows, f, mode)
+    S = np.array([np.asarray(g, dtype=np.float64).ravel() for g in sel])
+    beta = S.shape[0] - 2 * f
+    want = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j], beta) for j in range(S.shape[1])])
+    ties = np.array([orc.bulyan_boundary_tie(S[:, j], beta) for j in range(S.shape[1])])
+    return want, ties
+
+
+@pytest.mark.parametrize("rec", BY, ids=[r["name"] for r in BY])
+def test_golden_bulyan(rec):
+    xs = [rec["x"][i] for i in range(rec["x"].shape[0])]
+    p = rec["params"]
+    if "error" in rec:
+        with pytest.raises(IndexError):
+            gre.bulyan(xs, p["f"], p["aggsubfunc"])
+        return
+    got = gre.bulyan(xs, p["f"], p["aggsubfunc"])
+    assert got.dtype == np.float64 and got.shape == rec["out"].shape
+    want, ties = _leftfirst_and_ties(xs, p["f"], p["aggsubfunc"])
+    # 1. exactly the defined (left-first) tie rule everywhere
+    np.testing.assert_allclose(got.ravel(), want, rtol=1e-12, atol=1e-15)
+    # 2. the reference itself wherever its argsort order is not tie-dependent
+    ok = ~ties
+    np.testing.assert_allclose(got.ravel()[ok], rec["out"].ravel()[ok], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
+@pytest.mark.parametrize("n,f", [(100, 20), (64, 10), (37, 8)])
+def test_bulyan_against_oracle(mode, n, f):
+    x = make_rows(n, 1500, seed=77 + n + f, byz=f)
+    want, _ = _leftfirst_and_ties(list(x), f, mode)
+    got = engine.bulyan(torch.from_numpy(x).cuda(), f, mode).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)
+
+
+def test_bulyan_krum_selection_matches_oracle():
+    x = make_rows(60, 4000, seed=11, byz=12, identical_byz=True)
+    rows = [r for r in x]
+    _, removed = orc.bulyan_select(rows, 12, "krum")
+    _, sel = engine.bulyan(torch.from_numpy(x).cuda(), 12, "krum", selected=True)
+    assert sel.cpu().tolist() == removed
+
+
+def test_bulyan_even_theta_tiebreak_dense_ties():
+    # integer-valued data: many exact ties in distances and values
+    rng = np.random.default_rng(5)
+    x = rng.integers(-4, 5, size=(48, 700)).astype(np.float32)
+    for mode in ("krum", "median", "trimmedmean"):
+        want, _ = _leftfirst_and_ties(list(x), 10, mode)
+        got = engine.bulyan(torch.from_numpy(x).cuda(), 10, mode).cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)

@@ -73,3 +73,27 @@ def test_oracle_c1_convnet_round():
     np.testing.assert_array_equal(med, z["median"])
     np.testing.assert_array_equal(tm, z["trimmedmean"])
     assert json.loads(str(z["shapes"]))[4] == [200, 1470]
+
+
+def test_leftfirst_bulyan_rule_equals_reference_off_ties():
+    """The defined tie rule (oracle.bulyan_one_coordinate_leftfirst, which the
+    GPU kernel implements) reproduces the reference bit for bit on every
+    coordinate whose beta-nearest set is not tie-ambiguous."""
+    from conftest import fixtures
+    n_tie = 0
+    for rec in fixtures(func="bulyan"):
+        if "error" in rec:
+            continue
+        xs = [rec["x"][i] for i in range(rec["x"].shape[0])]
+        p = rec["params"]
+        rows = [np.asarray(r).ravel() for r in xs]
+        sel, _ = orc.bulyan_select(rows, p["f"], p["aggsubfunc"])
+        S = np.array([np.asarray(g, dtype=np.float64).ravel() for g in sel])
+        beta = S.shape[0] - 2 * p["f"]
+        for j in range(S.shape[1]):
+            tie = orc.bulyan_boundary_tie(S[:, j], beta)
+            n_tie += tie
+            if not tie:
+                got = orc.bulyan_one_coordinate_leftfirst(S[:, j], beta)
+                assert got == rec["out"].ravel()[j] or abs(got - rec["out"].ravel()[j]) <= 1e-15
+    assert n_tie > 0   # the median-mode fixtures do contain such ties
