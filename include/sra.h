@@ -138,6 +138,32 @@ int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32_t mode, si
 int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
                    int32_t* selected, void* ws, size_t ws_bytes, void* stream);
 
+
+/* ------------------------------------------------------------------------ */
+/* Spectral filters (k6)                                                     */
+/* ------------------------------------------------------------------------ */
+
+/* mode 0: robust_estimator.filterL2 (src/robust_estimator.py:144-208);
+ * mode 1: robust_estimator.ex_noregret (src/robust_estimator.py:42-133).
+ * The layer (n x d) is cut into itv-wide chunks (last one partial); each chunk
+ * is filtered in client space from its centred fp64-MFMA Gram (top eigenpair
+ * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 128.
+ * status: device int32, zeroed by the caller; set to 2 when an ex_noregret
+ * projection has no feasible candidate (the reference then fails with
+ * TypeError). */
+int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv, double eps,
+                   double sigma, double expansion, double* out, int32_t* status, void* stream);
+
+/* Diagnostics variant: as sra_filter_f32, and additionally writes chunk 0's
+ * centred Gram (128 x 128 fp64, row-major, zero-padded) followed by one record
+ * of 144 doubles per filter iteration (weights before the update [128], top
+ * eigenvalue, Lanczos steps, Ritz residual, restarts, 12 solver scalars) into dbg, which must hold
+ * SRA_FILTER_DEBUG_DOUBLES doubles. */
+#define SRA_FILTER_DEBUG_DOUBLES (128 * 128 + 256 * 144)
+int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
+                         double eps, double sigma, double expansion, double* out, int32_t* status, double* dbg,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

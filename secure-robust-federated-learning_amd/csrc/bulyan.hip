@@ -162,40 +162,6 @@ __global__ void __launch_bounds__(256) bulyan_pick_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 // per-coordinate Bulyan stage
 // ---------------------------------------------------------------------------
-// numpy pairwise fp64 sum of f(0..n) for n <= 128 (eight accumulators)
-template <typename F>
-__device__ __forceinline__ double np_pw_block64(int n, F&& f) {
-  if (n < 8) {
-    double res = 0.0;
-    for (int i = 0; i < n; ++i) res += f(i);
-    return res;
-  }
-  double r0 = f(0), r1 = f(1), r2 = f(2), r3 = f(3), r4 = f(4), r5 = f(5), r6 = f(6), r7 = f(7);
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-    r0 += f(i); r1 += f(i + 1); r2 += f(i + 2); r3 += f(i + 3);
-    r4 += f(i + 4); r5 += f(i + 5); r6 += f(i + 6); r7 += f(i + 7);
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += f(i);
-  return res;
-}
-
-template <typename F>
-__device__ __forceinline__ double np_pw64(int lo, int n, F&& f) {
-  if (n <= 128) return np_pw_block64(n, [&](int i) { return f(lo + i); });
-  int n2 = n / 2;
-  n2 -= n2 % 8;
-  auto half = [&](int l2, int m2) -> double {
-    if (m2 <= 128) return np_pw_block64(m2, [&](int i) { return f(l2 + i); });
-    int q = m2 / 2;
-    q -= q % 8;
-    return np_pw_block64(q, [&](int i) { return f(l2 + i); }) +
-           np_pw_block64(m2 - q, [&](int i) { return f(l2 + q + i); });
-  };
-  return half(lo, n2) + half(lo + n2, n - n2);
-}
-
 template <int P>  // theta <= P; 64-thread blocks (one wave), sorted columns in LDS
 __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
                                                           const int* __restrict__ rows, int theta, int beta,

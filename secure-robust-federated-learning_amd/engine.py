@@ -174,3 +174,78 @@ def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
     _lib.call("sra_bulyan_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
               sel.data_ptr() if sel is not None else None, ws.data_ptr(), nb, _stream_ptr(X.device))
     return (out, sel) if selected else out
+
+
+# ---------------------------------------------------------------------------
+# spectral filters
+# ---------------------------------------------------------------------------
+ITV = 1000
+
+
+def chunk_width(d, itv):
+    """robust_estimator.py:116-117, 192-193: itv None -> floor(sqrt(d))."""
+    if itv is None:
+        import math
+        return int(math.floor(math.sqrt(d)))
+    return int(itv)
+
+
+def _filter(X, mode, eps, sigma, expansion, itv, check):
+    X, n, d, ldx = as_matrix(X)
+    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    status = torch.zeros(1, dtype=torch.int32, device=X.device)
+    _lib.call("sra_filter_f32", X.data_ptr(), n, d, ldx, int(mode), chunk_width(d, itv), float(eps), float(sigma),
+              float(expansion), out.data_ptr(), status.data_ptr(), _stream_ptr(X.device))
+    if check and int(status.item()) == 2:
+        raise TypeError("ex_noregret: no feasible capped-simplex projection (projected_c is None)")
+    return out
+
+
+FILTER_DEBUG_DOUBLES = 128 * 128 + 256 * 144
+
+
+def filter_debug(X, mode, eps, sigma, expansion, itv):
+    """Run a filter and return (out, G0, records) for chunk 0: G0 the centred
+    chunk Gram (n x n fp64), records an (iters, 144) array of
+    [weights(128), lambda, lanczos_steps, ritz_residual, restarts, 12 solver scalars]."""
+    X, n, d, ldx = as_matrix(X)
+    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    status = torch.zeros(1, dtype=torch.int32, device=X.device)
+    dbg = torch.full((FILTER_DEBUG_DOUBLES,), float("nan"), dtype=torch.float64, device=X.device)
+    _lib.call("sra_filter_debug_f32", X.data_ptr(), n, d, ldx, int(mode), chunk_width(d, itv), float(eps),
+              float(sigma), float(expansion), out.data_ptr(), status.data_ptr(), dbg.data_ptr(),
+              _stream_ptr(X.device))
+    dbg = dbg.cpu()
+    G = dbg[:128 * 128].reshape(128, 128)[:n, :n].clone()
+    recs = dbg[128 * 128:].reshape(256, 144)
+    return out, G, recs
+
+
+def filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, check=True):
+    """robust_estimator.filterL2 on device: float64 (d,)."""
+    return _filter(X, 0, eps, sigma, expansion, itv, check)
+
+
+def ex_noregret(X, eps=1. / 12, sigma=1, expansion=20, itv=ITV, check=True):
+    """robust_estimator.ex_noregret on device: float64 (d,)."""
+    return _filter(X, 1, eps, sigma, expansion, itv, check)
+
+
+def mom_bucket_count(n, eps, delta):
+    """robust_estimator.py:136-137 / 211-212, evaluated in float64 like numpy."""
+    import math
+    num = int(math.floor(eps * n) + math.log(1. / delta))
+    size = int(math.ceil(n * 1. / num))
+    return num, size
+
+
+def mom_filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True):
+    n = int(X.shape[0])
+    num, size = mom_bucket_count(n, eps, delta)
+    return filter_l2(bucket_means(X, size, num), eps, sigma, expansion, itv, check)
+
+
+def mom_ex_noregret(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True):
+    n = int(X.shape[0])
+    num, size = mom_bucket_count(n, eps, delta)
+    return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check)

@@ -142,3 +142,44 @@ def bulyan(grads, f, aggsubfunc="trimmedmean"):
     """robust_estimator.py:277-332 (float64 result, like the reference)."""
     st = _stage(grads)
     return st.result(engine.bulyan(st.X, f, aggsubfunc), dtype=np.float64)
+
+
+# ---------------------------------------------------------------------------
+# spectral filters
+# ---------------------------------------------------------------------------
+def filterL2_(samples, eps=0.2, sigma=1, expansion=20):
+    """robust_estimator.py:144-177 on one (n, k) chunk."""
+    st = _stage(samples)
+    k = int(st.X.shape[1])
+    return st.result(engine.filter_l2(st.X, eps, sigma, expansion, itv=k), dtype=np.float64)
+
+
+def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV):
+    """robust_estimator.py:180-208."""
+    st = _stage(samples)
+    return st.result(engine.filter_l2(st.X, eps, sigma, expansion, itv), dtype=np.float64)
+
+
+def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
+    """robust_estimator.py:210-218."""
+    st = _stage(samples)
+    return st.result(engine.mom_filter_l2(st.X, eps, sigma, expansion, itv, delta), dtype=np.float64)
+
+
+def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7):
+    """robust_estimator.py:42-102 on one (n, k) chunk."""
+    st = _stage(samples)
+    k = int(st.X.shape[1])
+    return st.result(engine.ex_noregret(st.X, eps, sigma, expansion, itv=k), dtype=np.float64)
+
+
+def ex_noregret(samples, eps=1. / 12, sigma=1, expansion=20, itv=ITV):
+    """robust_estimator.py:104-133."""
+    st = _stage(samples)
+    return st.result(engine.ex_noregret(st.X, eps, sigma, expansion, itv), dtype=np.float64)
+
+
+def mom_ex_noregret(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
+    """robust_estimator.py:135-142."""
+    st = _stage(samples)
+    return st.result(engine.mom_ex_noregret(st.X, eps, sigma, expansion, itv, delta), dtype=np.float64)

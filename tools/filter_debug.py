@@ -1,0 +1,37 @@
+"""Dump the spectral-filter diagnostics of a golden fixture (GPU box helper)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import srfl_loader  # noqa: E402
+
+srfl_loader.load()
+from srfl_amd import engine  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "filterL2_exit"
+z = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
+import json
+p = json.loads(str(z["params"]))
+x = z["x"].reshape(z["x"].shape[0], -1)
+mode = 1 if "noregret" in name else 0
+itv = p["itv"] or int(np.floor(np.sqrt(x.shape[1])))
+out, G, recs = engine.filter_debug(torch.from_numpy(np.ascontiguousarray(x)).cuda(), mode, p["eps"], p["sigma"],
+                                   p["expansion"], itv)
+np.set_printoptions(precision=6, linewidth=160)
+ch = x[:, :itv].astype(np.float64)
+zc = ch - ch.mean(0)
+print("G err", np.abs(G.numpy() - zc @ zc.T).max(), "G max", np.abs(zc @ zc.T).max())
+print("G diag", np.diag(G.numpy())[:8])
+n = x.shape[0]
+for it in range(recs.shape[0]):
+    r = recs[it].numpy()
+    if np.isnan(r[128]) and np.isnan(r[0]):
+        break
+    print("it", it, "lam", r[128], "m", r[129], "resid", r[130], "rs", r[131], "c", r[:min(n, 8)])
+    print("    scal4..15", r[132:144])
+print("out", out.cpu().numpy()[:8])
+print("want", z["out"].ravel()[:8] if "out" in z else None)
