@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--agg", default="trimmedmean", choices=["trimmedmean", "median", "average", "krum", "mom_krum"])
+    ap.add_argument("--agg", default="trimmedmean",
+                    choices=["trimmedmean", "median", "average", "krum", "mom_krum", "bulyankrum", "bulyanmedian",
+                             "bulyantrimmedmean", "filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"])
     ap.add_argument("--clients", type=int, default=128)
     ap.add_argument("--d", type=float, default=1e8, help="coordinates per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -69,45 +71,116 @@ def _mom_krum_step(X, out):
     out.copy_(row)
 
 
+def _bulyan_step(mode):
+    def step(X, out):
+        out.copy_(engine.bulyan(X, 20, mode))
+    return step
+
+
+# simulate.py defaults (SURVEY.md §8 convention): f=20, eps=0.2, sigma=1e-5,
+# expansion=20, itv=1000; for MoM the delta of config C5 (e^-26).
+FILTER_ARGS = dict(eps=0.2, sigma=1e-5, expansion=20, itv=1000)
+MOM_DELTA = 2.718281828459045 ** -26
+
+
+def _filter_step(fn, mom=False):
+    def step(X, out):
+        if mom:
+            out.copy_(fn(X, delta=MOM_DELTA, check=False, **FILTER_ARGS))
+        else:
+            out.copy_(fn(X, check=False, **FILTER_ARGS))
+    return step
+
+
 AGG = {
     "trimmedmean": lambda X, out: engine.trimmed_mean(X, 0.1, out=out),
     "median": lambda X, out: engine.median(X, out=out),
     "average": lambda X, out: engine.average(X, out=out),
     "krum": _krum_step,
     "mom_krum": _mom_krum_step,
+    "bulyankrum": _bulyan_step("krum"),
+    "bulyanmedian": _bulyan_step("median"),
+    "bulyantrimmedmean": _bulyan_step("trimmedmean"),
+    "filterl2": _filter_step(engine.filter_l2),
+    "ex_noregret": _filter_step(engine.ex_noregret),
+    "mom_filterl2": _filter_step(engine.mom_filter_l2, mom=True),
+    "mom_ex_noregret": _filter_step(engine.mom_ex_noregret, mom=True),
 }
+OUT_DTYPE = {"bulyankrum": torch.float64, "bulyanmedian": torch.float64, "bulyantrimmedmean": torch.float64,
+             "filterl2": torch.float64, "ex_noregret": torch.float64, "mom_filterl2": torch.float64,
+             "mom_ex_noregret": torch.float64}
 KERNEL_NAME = {
     "trimmedmean": "select_reg_kernel<128, 1, 128, 12>",
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
-    "krum": "whole krum op (gram_partial_kernel<4> dominant; per-kernel split in profiles/)",
+    "krum": "whole krum op (gram_partial_kernel dominant; per-kernel split in profiles/)",
     "mom_krum": "whole mom_krum op (bucket means + Gram + scoring)",
+    "bulyankrum": "whole bulyan op (Gram + theta Krum rounds + final stage)",
+    "bulyanmedian": "whole bulyan op (theta select+distance rounds + final stage)",
+    "bulyantrimmedmean": "whole bulyan op (theta select+distance rounds + final stage)",
+    "filterl2": "spectral_filter_kernel<0> (chunk Gram on fp64 MFMA + client-space solver)",
+    "ex_noregret": "spectral_filter_kernel<1> (chunk Gram on fp64 MFMA + client-space solver)",
+    "mom_filterl2": "whole op (bucket means + spectral_filter_kernel<0>)",
+    "mom_ex_noregret": "whole op (bucket means + spectral_filter_kernel<1>)",
 }
-MFMA_PEAK_TFLOPS = 157.3  # fp32 MFMA (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = 157.3      # fp32 MFMA (MI355X_MICROARCH.md)
+MFMA64_PEAK_TFLOPS = 78.6     # fp64 MFMA
+
+
+def roofline_model(agg, n, d):
+    """(bound, peak, unit, algorithmic amount per launch) — SURVEY.md §8(d)."""
+    if agg in ("trimmedmean", "median", "average"):
+        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
+    if agg in ("krum", "mom_krum", "bulyankrum"):
+        m = n if agg != "mom_krum" else -(-n // 3)
+        return "mfma", MFMA_PEAK_TFLOPS, "TFLOP/s", m * (m + 1) * d
+    if agg in ("bulyanmedian", "bulyantrimmedmean"):
+        theta = n - 40
+        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * d * sum(n - i for i in range(theta)) + 8 * theta * d + 4 * d
+    if agg in ("filterl2", "ex_noregret"):
+        return "mfma", MFMA64_PEAK_TFLOPS, "TFLOP/s", n * (n + 1) * d
+    # MoM filters: bucket pass (HBM) dominates at C5 (SURVEY.md §8(d))
+    return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
 
 
 def cpu_baseline(agg, n, budget_s):
-    """Time the oracle's CPU port on N x 1e6 chunks until ~budget_s elapsed."""
+    """Time the oracle's CPU port on a bounded sample until ~budget_s elapsed."""
     from oracle import robust_np as orc
+    fa = FILTER_ARGS
     fn = {"trimmedmean": orc.trimmed_mean, "median": orc.median, "average": orc.average,
-          "krum": lambda xs: orc.krum(xs, 20), "mom_krum": lambda xs: orc.mom_krum(xs, 20)}[agg]
-    d = 1_000_000 if agg not in ("krum", "mom_krum") else 100_000
+          "krum": lambda xs: orc.krum(xs, 20), "mom_krum": lambda xs: orc.mom_krum(xs, 20),
+          "bulyankrum": lambda xs: orc.bulyan(xs, 20, "krum"),
+          "bulyanmedian": lambda xs: orc.bulyan(xs, 20, "median"),
+          "bulyantrimmedmean": lambda xs: orc.bulyan(xs, 20, "trimmedmean"),
+          "filterl2": lambda xs: orc.filterL2(xs, fa["eps"], fa["sigma"], fa["expansion"], fa["itv"]),
+          "ex_noregret": lambda xs: orc.ex_noregret(xs, fa["eps"], fa["sigma"], fa["expansion"], fa["itv"]),
+          "mom_filterl2": lambda xs: orc.mom_filterL2(xs, fa["eps"], fa["sigma"], fa["expansion"], fa["itv"],
+                                                      MOM_DELTA),
+          "mom_ex_noregret": lambda xs: orc.mom_ex_noregret(xs, fa["eps"], fa["sigma"], fa["expansion"],
+                                                            fa["itv"], MOM_DELTA)}[agg]
+    d = {"krum": 100_000, "mom_krum": 100_000, "bulyankrum": 2_000, "bulyanmedian": 2_000,
+         "bulyantrimmedmean": 2_000, "filterl2": 1000, "ex_noregret": 1000, "mom_filterl2": 1000,
+         "mom_ex_noregret": 1000}.get(agg, 1_000_000)
     rng = np.random.default_rng(0)
     x = (0.01 * rng.standard_normal((n, d))).astype(np.float32)
     samples = list(x)
-    fn(samples)  # warm
     t0 = time.perf_counter()
-    reps = 0
-    while True:
-        fn(samples)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 200:
-            break
+    fn(samples)  # warm (also the sample itself when one call is slow)
+    first = time.perf_counter() - t0
+    reps, el = 1, first
+    if first < budget_s / 3:
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            fn(samples)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or reps >= 200:
+                break
     gbs = reps * n * d * 4 / el / 1e9
-    return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "%d x numpy %s over N=%d x d=1e6 fp32 (oracle/robust_np.py), %.1f s on host cores, single thread"
-                      % (reps, agg, n, el)}
+    return {"value": round(gbs, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "%d x numpy %s over N=%d x d=%d fp32 (oracle/robust_np.py), %.1f s on host cores, "
+                      "single thread" % (reps, agg, n, d, el)}
 
 
 def host_inclusive(agg, n, device):
@@ -115,9 +188,9 @@ def host_inclusive(agg, n, device):
     d = 4_000_000
     host = torch.empty((n, d), dtype=torch.float32, pin_memory=True)
     host.normal_(0, 0.01)
-    res = torch.empty(d, dtype=torch.float32, pin_memory=True)
+    res = torch.empty(d, dtype=OUT_DTYPE.get(agg, torch.float32), pin_memory=True)
     X = torch.empty((n, d), dtype=torch.float32, device=device)
-    out = torch.empty(d, dtype=torch.float32, device=device)
+    out = torch.empty(d, dtype=OUT_DTYPE.get(agg, torch.float32), device=device)
     for _ in range(2):
         X.copy_(host, non_blocking=True); AGG[agg](X, out); res.copy_(out, non_blocking=True)
     torch.cuda.synchronize()
@@ -150,8 +223,9 @@ def main():
     rows_per = max(1, int(2e9 // (4 * d)) or 1)
     for r0 in range(0, n, rows_per):
         X[r0:r0 + rows_per].normal_(0.0, 0.01, generator=g)
-    out = torch.empty(d, dtype=torch.float32, device=device)
-    full = torch.empty(d * world, dtype=torch.float32, device=device) if world > 1 else None
+    odt = OUT_DTYPE.get(a.agg, torch.float32)
+    out = torch.empty(d, dtype=odt, device=device)
+    full = torch.empty(d * world, dtype=odt, device=device) if world > 1 else None
     fn = AGG[a.agg]
 
     def step(ev=None):
@@ -186,14 +260,9 @@ def main():
     total_bytes = n * d * world * 4
     value = total_bytes / (elapsed / a.steps) / 1e9
 
-    alg_bytes = 4 * n * d + 4 * d
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
-    if a.agg in ("krum", "mom_krum"):
-        m = n if a.agg == "krum" else -(-n // 3)
-        flops = m * (m + 1) * d            # upper-triangle centred Gram, 2 flops per FMA
-        bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS, "TFLOP/s"
-        achieved = flops / (kern_ms * 1e-3) / 1e12
+    bound, peak, unit, alg = roofline_model(a.agg, n, d)
+    scale = 1e9 if unit == "GB/s" else 1e12
+    achieved = alg / (kern_ms * 1e-3) / scale
     traffic = None
     try:
         with open(a.traffic_json) as fh:
@@ -223,7 +292,7 @@ def main():
         "roofline": {"bound": bound, "kernel": KERNEL_NAME[a.agg], "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic, "kernel_ms": round(kern_ms, 4),
-                     "algorithmic_bytes_per_launch": alg_bytes},
+                     ("algorithmic_bytes_per_launch" if unit == "GB/s" else "algorithmic_flops_per_launch"): alg},
     }
     if rank == 0 and world == 1 and not a.no_host:
         del X

@@ -40,7 +40,8 @@ namespace sra {
 constexpr int FNP = 128;           // padded client count
 constexpr int FST = 64;            // coordinates per Gram stage
 constexpr int FROW = FST + 4;      // stage row stride (floats)
-constexpr int LMAX = 64;           // Lanczos steps per restart (V fills the 64 KB union)
+constexpr int LMAX = 62;           // Lanczos steps per restart (V fills the 64 KB union)
+constexpr int VST = FNP + 4;       // Lanczos basis row stride (doubles): spreads rows over LDS banks
 constexpr int LRESTART = 6;        // explicit restarts from the Ritz vector
 
 struct FilterShared {
@@ -70,12 +71,40 @@ struct FilterArgs {
 // steps, Ritz residual, restarts used, then 12 solver scalars (scal[4..15]).
 constexpr int kDbgRec = 128 + 16;
 
-// ----- block helpers (256 threads) ------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+// ----- wave / block helpers (256 threads) --------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), l);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), l);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+// v with lane l replaced by x (l uniform)
+__device__ __forceinline__ double writelane_f64(double x, int l, double v) {
+  return static_cast<int>(threadIdx.x & 63) == l ? x : v;
+}
+// sum over the wave, identical in every lane (DPP within rows, readlane across)
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  v = fmax(v, dpp_f64<0x140>(v));
+  return fmax(fmax(readlane_f64(v, 0), readlane_f64(v, 16)), fmax(readlane_f64(v, 32), readlane_f64(v, 48)));
+}
+__device__ __forceinline__ double wave_min(double v) { return -wave_max(-v); }
 __device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -110,19 +139,6 @@ __device__ float np_pw32(int n, F&& f) {
   int n2 = n / 2;
   n2 -= n2 % 8;
   return block(0, n2) + block(n2, n - n2);
-}
-
-// ----- Sturm count: eigenvalues of the tridiagonal (a, b) below x ------------
-__device__ __forceinline__ int sturm_count(const double* a, const double* b, int m, double x) {
-  int cnt = 0;
-  double dd = a[0] - x;
-  if (dd < 0) ++cnt;
-  for (int k = 1; k < m; ++k) {
-    const double den = (dd == 0.0) ? 1e-300 : dd;
-    dd = (a[k] - x) - b[k - 1] * b[k - 1] / den;
-    if (dd < 0) ++cnt;
-  }
-  return cnt;
 }
 
 // 36 upper-triangle 16x16 tiles (I <= J) of the 128 x 128 chunk Gram
@@ -195,29 +211,110 @@ __device__ __forceinline__ void filter_gram_phase(const FilterArgs& A, int64_t k
   }
 }
 
+// ----- block reductions (256 threads = 4 waves) -------------------------------
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wave] = a;
+    red[4 + wave] = b;
+  }
+  __syncthreads();
+  a = (red[0] + red[1]) + (red[2] + red[3]);
+  b = (red[4] + red[5]) + (red[6] + red[7]);
+  __syncthreads();
+}
+
+// index of the largest v (first index on ties); inactive lanes pass -inf.
+// Returns the index; *vbest receives its value.
+__device__ __forceinline__ int block_argmax_first(double v, int i, double* red, int* ired, double* vbest) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const int oi = __shfl_xor(i, off);
+    if (ov > v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wave] = v;
+    ired[wave] = i;
+  }
+  __syncthreads();
+  double bv = red[0];
+  int bi = ired[0];
+  for (int q = 1; q < 4; ++q)
+    if (red[q] > bv || (red[q] == bv && ired[q] < bi)) {
+      bv = red[q];
+      bi = ired[q];
+    }
+  __syncthreads();
+  *vbest = bv;
+  return bi;
+}
+
+__device__ __forceinline__ int block_min_int(int v, int* ired) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) ired[4 + wave] = v;
+  __syncthreads();
+  int r = ired[4];
+  for (int q = 5; q < 8; ++q) r = ired[q] < r ? ired[q] : r;
+  __syncthreads();
+  return r;
+}
+
+// Sturm count with a Newton-refined reciprocal instead of a full division
+__device__ __forceinline__ int sturm_count_fast(const double* a, const double* b2, int m, double x, double tiny) {
+  int cnt = 0;
+  double dd = a[0] - x;
+  for (int k = 0; k < m; ++k) {
+    if (k > 0) {
+      double r = __builtin_amdgcn_rcp(dd);
+      r = r * (2.0 - dd * r);
+      dd = (a[k] - x) - b2[k - 1] * r;
+    }
+    if (fabs(dd) < tiny) dd = -tiny;
+    if (dd < 0) ++cnt;
+  }
+  return cnt;
+}
+
 template <int MODE>  // 0: filterL2, 1: ex_noregret
-__global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
+__global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* uni = smem;                                     // 64 KB union
   double* vec = reinterpret_cast<double*>(smem + FilterShared::kUnionBytes);
-  double* c = vec;                 // weights (kept/active clients)
+  double* c = vec;                 // weights (active clients)
   double* w = vec + 1 * FNP;       // normalised weights
   double* sw = vec + 2 * FNP;      // sqrt(w)
   double* gw = vec + 3 * FNP;      // G w
-  double* xv = vec + 4 * FNP;      // Lanczos work vector / generic input
-  double* yv = vec + 5 * FNP;      // output of the operator
-  double* rv = vec + 6 * FNP;      // Lanczos residual
+  double* xv = vec + 4 * FNP;      // operator input (sw o vector)
+  double* yv = vec + 5 * FNP;      // G xv
+  double* rv = vec + 6 * FNP;      // Lanczos residual / scratch
   double* uv = vec + 7 * FNP;      // Ritz vector (warm start)
-  double* tau = vec + 8 * FNP;
-  double* alpha = vec + 9 * FNP;             // [LMAX]
-  double* beta = alpha + LMAX;               // [LMAX]
-  double* svec = beta + LMAX;                // [LMAX] eigenvector of T
-  double* red = svec + LMAX;                 // [8]
-  double* scal = red + 8;                    // [16] broadcast scalars
-  double* tcp = scal + 16;                   // [LMAX] tridiagonal solve scratch
-  double* tdp = tcp + LMAX;                  // [LMAX]
-  int* active = reinterpret_cast<int*>(tdp + LMAX);   // [FNP]
-  int* iscal = active + FNP;                          // [16]
+  double* tau = vec + 8 * FNP;     // outlier scores / Krum scores
+  double* sv = yv;                 // ex_noregret projection: weights in descending order
+  double* hl = xv;                 // ex_noregret projection: sv * log(sv / cap)
+  double* alpha = vec + 9 * FNP;   // [LMAX]
+  double* beta = alpha + LMAX;     // [LMAX]
+  double* beta2 = beta + LMAX;     // [LMAX] beta^2 (Sturm)
+  double* svec = beta2 + LMAX;     // [LMAX] eigenvector of T
+  double* hq = svec + LMAX;        // [LMAX] re-orthogonalisation coefficients
+  double* tcp = hq + LMAX;         // [LMAX] tridiagonal solve scratch
+  double* red = tcp + LMAX;        // [16]
+  double* scal = red + 16;         // [16] broadcast scalars
+  int* active = reinterpret_cast<int*>(scal + 16);  // [FNP]
+  int* kidx = active + FNP;                         // [FNP] compact -> client
+  int* irank = kidx + FNP;                          // [FNP] descending rank of compact entry
+  int* iscal = irank + FNP;                         // [16]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -225,6 +322,7 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
   const int n = A.n;
   const int grow = tid >> 1;   // G row owned by this thread
   const int ghalf = tid & 1;   // which 64 columns
+  const bool own = tid < FNP;  // thread owns client tid
 
   for (int chunk = blockIdx.x; chunk < A.nchunks; chunk += gridDim.x) {
     const int64_t k0 = static_cast<int64_t>(chunk) * A.itv;
@@ -262,35 +360,45 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
       }
       __syncthreads();
     }
-
     const bool dbg = A.dbg != nullptr && chunk == 0;
     if (dbg) {
 #pragma unroll
       for (int j = 0; j < 64; ++j) A.dbg[grow * FNP + 64 * ghalf + j] = g[j];
     }
 
-    // operator helpers -------------------------------------------------------
-    // yv = G * xv  (all rows)
-    auto gmv = [&](const double* x, double* y) {
-      double p = 0.0;
+    // y = G x for x in LDS; every thread of the row pair gets the row value
+    auto gmv_row = [&](const double* x) -> double {
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+      const double* xh = x + 64 * ghalf;
 #pragma unroll
-      for (int j = 0; j < 64; ++j) p += g[j] * x[64 * ghalf + j];
-      p += __shfl_xor(p, 1);
-      if (ghalf == 0) y[grow] = p;
-      __syncthreads();
-    };
-    // y = C (sw o x) [post-scaled by sw if scale_out]; s_gw = w^T G w in scal[0]
-    auto cop = [&](const double* x, double* y, bool scale_out) {
-      if (tid < FNP) xv[tid] = sw[tid] * x[tid];
-      __syncthreads();
-      const double s1 = block_sum(tid < FNP ? xv[tid] : 0.0, red);
-      const double gy = block_sum(tid < FNP ? gw[tid] * xv[tid] : 0.0, red);
-      gmv(xv, yv);
-      if (tid < FNP) {
-        const double cy = yv[tid] - gw[tid] * s1 - gy + scal[0] * s1;
-        y[tid] = scale_out ? sw[tid] * cy : cy;
+      for (int j = 0; j < 64; j += 4) {
+        p0 += g[j] * xh[j];
+        p1 += g[j + 1] * xh[j + 1];
+        p2 += g[j + 2] * xh[j + 2];
+        p3 += g[j + 3] * xh[j + 3];
       }
+      const double p = (p0 + p1) + (p2 + p3);
+      return p + dpp_f64<0xB1>(p);   // the row's other half lives in lane ^ 1
+    };
+    // (C xv)[tid] for the owning threads, C = G - g1' - 1g' + s11' with
+    // g = gw, s = scal[0]; xv must be visible.  Two barriers.
+    auto cmul = [&]() -> double {
+      const double p = gmv_row(xv);
+      double a1 = own ? xv[tid] : 0.0;
+      double a2 = own ? gw[tid] * xv[tid] : 0.0;
+      a1 = wave_sum(a1);
+      a2 = wave_sum(a2);
+      if (lane == 0) {
+        red[wave] = a1;
+        red[4 + wave] = a2;
+      }
+      if (ghalf == 0) yv[grow] = p;
       __syncthreads();
+      const double s1 = (red[0] + red[1]) + (red[2] + red[3]);
+      const double gy = (red[4] + red[5]) + (red[6] + red[7]);
+      const double r = own ? yv[tid] - gw[tid] * s1 - gy + scal[0] * s1 : 0.0;
+      __syncthreads();
+      return r;
     };
 
     // ============ ex_noregret: Krum pre-filter on the chunk =================
@@ -298,8 +406,7 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
     double step = 0.0;
     if constexpr (MODE == 1) {
       const int fp = static_cast<int>(ceil(A.eps * n));
-      float* drow = reinterpret_cast<float*>(uni);   // [FNP][FNP] fp32 distances, row i sorted later
-      // diag of G into xv (compile-time register indices only)
+      float* drow = reinterpret_cast<float*>(uni);   // [FNP][FNP] fp32 distances
       {
         double dg = 0.0;
 #pragma unroll
@@ -308,7 +415,6 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
         if ((grow >> 6) == ghalf) xv[grow] = dg;
       }
       __syncthreads();
-      // fill distances from the register rows: thread (row, half) writes its 64 entries
       for (int j = 0; j < 64; ++j) {
         const int col = 64 * ghalf + j;
         if (grow < n && col < n) {
@@ -317,47 +423,64 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
         }
       }
       __syncthreads();
-      // per row: sort the n-1 off-diagonal distances (insertion sort, one lane
-      // per row) and score with numpy's pairwise fp32 sum of the m smallest
+      // each wave sorts whole rows (the n-1 off-diagonal distances, +inf
+      // padded to 128) with a register bitonic network, 2 elements per lane
+      for (int row = wave; row < n; row += 4) {
+        auto ld = [&](int e) -> float {
+          if (e >= n - 1) return __builtin_inff();
+          return drow[row * FNP + (e < row ? e : e + 1)];
+        };
+        float v0 = ld(2 * lane), v1 = ld(2 * lane + 1);
+#pragma unroll
+        for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+          for (int stride = size >> 1; stride >= 1; stride >>= 1) {
+            const bool asc = ((2 * lane) & size) == 0;
+            if (stride == 1) {
+              const float lo = fminf(v0, v1), hi = fmaxf(v0, v1);
+              v0 = asc ? lo : hi;
+              v1 = asc ? hi : lo;
+            } else {
+              const int ls = stride >> 1;
+              const float p0 = __shfl_xor(v0, ls), p1 = __shfl_xor(v1, ls);
+              const bool takemin = asc != ((lane & ls) != 0);
+              v0 = takemin ? fminf(v0, p0) : fmaxf(v0, p0);
+              v1 = takemin ? fminf(v1, p1) : fmaxf(v1, p1);
+            }
+          }
+        }
+        drow[row * FNP + 2 * lane] = v0;
+        drow[row * FNP + 2 * lane + 1] = v1;
+      }
+      __syncthreads();
+      // score = numpy pairwise fp32 sum of the m smallest (slice semantics)
       const int m = n - fp - 2 >= 0 ? (n - fp - 2 < n - 1 ? n - fp - 2 : n - 1)
                                     : ((n - 1) + (n - fp - 2) > 0 ? (n - 1) + (n - fp - 2) : 0);
       if (tid < n) {
-        float* row = drow + tid * FNP;
-        // move the diagonal out: compact to n-1 entries
-        int p = 0;
-        for (int j = 0; j < n; ++j)
-          if (j != tid) row[p++] = row[j];
-        for (int a = 1; a < n - 1; ++a) {
-          const float v = row[a];
-          int b = a - 1;
-          while (b >= 0 && row[b] > v) {
-            row[b + 1] = row[b];
-            --b;
-          }
-          row[b + 1] = v;
-        }
+        const float* row = drow + tid * FNP;
         tau[tid] = static_cast<double>(np_pw32(m, [&](int q) { return row[q]; }));
       }
       __syncthreads();
-      // drop the fp largest scores (ties: later index dropped first, like a
-      // stable partition from the top)
-      if (tid < FNP) active[tid] = tid < n ? 1 : 0;
-      __syncthreads();
-      if (tid == 0) {
-        for (int r = 0; r < fp && r < n; ++r) {
-          int best = -1;
-          double bv = -1.0;
-          for (int i = 0; i < n; ++i)
-            if (active[i] && (best < 0 || tau[i] >= bv)) { bv = tau[i]; best = i; }
-          if (best >= 0) active[best] = 0;
+      // drop the fp largest scores (ties: later index dropped first)
+      if (own) {
+        int keep = 0;
+        if (tid < n) {
+          const double si = tau[tid];
+          int above = 0;
+          for (int j = 0; j < n; ++j) above += (tau[j] > si || (tau[j] == si && j > tid)) ? 1 : 0;
+          keep = above >= fp ? 1 : 0;
         }
-        int cnt = 0;
-        for (int i = 0; i < n; ++i) cnt += active[i];
-        iscal[0] = cnt;
+        active[tid] = keep;
       }
       __syncthreads();
-      n_keep = iscal[0];
-      // max pairwise distance (fp32, from the unsorted definition) among kept
+      // compaction of the kept clients (client order)
+      if (own && active[tid]) {
+        int pos = 0;
+        for (int j = 0; j < tid; ++j) pos += active[j];
+        kidx[pos] = tid;
+      }
+      n_keep = n - (fp < n ? fp : n);
+      // max pairwise fp32 distance among kept clients
       float md = 0.f;
       for (int j = 0; j < 64; ++j) {
         const int col = 64 * ghalf + j;
@@ -377,12 +500,11 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
       float mdall = static_cast<float>(red[0]);
       for (int q = 1; q < 4; ++q) mdall = static_cast<float>(red[q]) > mdall ? static_cast<float>(red[q]) : mdall;
       __syncthreads();
-      const float sq32 = mdall * mdall;
-      step = static_cast<double>(0.5f / sq32);
-      if (tid < FNP) c[tid] = (tid < n && active[tid]) ? 1.0 : 0.0;
+      step = static_cast<double>(0.5f / (mdall * mdall));
+      if (own) c[tid] = (tid < n && active[tid]) ? 1.0 : 0.0;
       __syncthreads();
     } else {
-      if (tid < FNP) {
+      if (own) {
         active[tid] = tid < n ? 1 : 0;
         c[tid] = tid < n ? 1.0 : 0.0;
       }
@@ -393,301 +515,350 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
     const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n)
                                 : static_cast<int>(2 * A.eps * n_keep);
     bool have_u = false;
+    int m_hint = 0;   // Lanczos steps the previous iteration needed
+    double* V = reinterpret_cast<double*>(uni);   // [LMAX][VST] Lanczos basis
     for (int it = 0; it < iters; ++it) {
-      // weights
-      const double csum = block_sum(tid < FNP && active[tid] ? c[tid] : 0.0, red);
-      if (tid < FNP) {
-        const double wi = active[tid] ? c[tid] / csum : 0.0;
+      // weights, G w, w'Gw, number of active clients
+      double csum = own && active[tid] ? c[tid] : 0.0;
+      csum = block_sum(csum, red);
+      double wi = 0.0;
+      if (own) {
+        wi = active[tid] ? c[tid] / csum : 0.0;
         w[tid] = wi;
         sw[tid] = sqrt(wi > 0.0 ? wi : 0.0);
       }
       __syncthreads();
-      gmv(w, gw);
       {
-        const double s = block_sum(tid < FNP ? w[tid] * gw[tid] : 0.0, red);
-        if (tid == 0) {
-          scal[0] = s;
-          if (dbg) { scal[4] = csum; scal[5] = s; scal[6] = gw[0]; scal[7] = sw[0]; }
-        }
-        __syncthreads();
+        const double p = gmv_row(w);
+        if (ghalf == 0) gw[grow] = p;
       }
-      // ---- Lanczos on M = W^1/2 C W^1/2 ----
-      int nact = 0;
-      {
-        const double cnt = block_sum(tid < FNP && sw[tid] > 0.0 ? 1.0 : 0.0, red);
-        nact = static_cast<int>(cnt);
-      }
-      int msteps = nact < LMAX ? nact : LMAX;
-      if (msteps < 1) msteps = 1;
-      double* V = reinterpret_cast<double*>(uni);   // [LMAX][FNP]
+      double sacc = 0.0, cnt = own && wi > 0.0 ? 1.0 : 0.0;
+      __syncthreads();
+      sacc = own ? wi * gw[tid] : 0.0;
+      block_sum2(sacc, cnt, red);
+      if (tid == 0) scal[0] = sacc;
+      const int nact = static_cast<int>(cnt);
+      __syncthreads();
+
+      // ---- top eigenpair of M = W^1/2 C W^1/2: Lanczos, full reorth ----
+      const int msteps = nact < 1 ? 1 : (nact < LMAX ? nact : LMAX);
       double lam = 0.0, resid_last = 0.0;
       int rs_used = 0, m_last = 0;
+      long long tm[6] = {0, 0, 0, 0, 0, 0};   // cycle probes (diagnostics only)
+      long long t0c = clock64();
 #pragma unroll 1
       for (int rs = 0; rs < LRESTART; ++rs) {
-      // start vector: previous Ritz vector (warm; perturbed towards sqrt-weights
-      // on a new outer iteration so no active client is missed) or sqrt-weights
-      if (tid < FNP)
-        rv[tid] = (sw[tid] > 0.0) ? (rs > 0 ? uv[tid] : (have_u ? uv[tid] + 1e-3 * sw[tid] : sw[tid])) : 0.0;
-      __syncthreads();
-      {
-        const double nrm = sqrt(block_sum(tid < FNP ? rv[tid] * rv[tid] : 0.0, red));
-        if (tid < FNP) V[tid] = rv[tid] / nrm;
-        if (dbg && tid == 0 && rs == 0) { scal[8] = nrm; scal[9] = rv[0]; }
-        __syncthreads();
-      }
-      int mused = msteps;
-      for (int j = 0; j < msteps; ++j) {
-        double* qj = V + j * FNP;
-        cop(qj, rv, true);     // rv = M q_j
-        const double aj = block_sum(tid < FNP ? qj[tid] * rv[tid] : 0.0, red);
-        if (tid < FNP) {
-          double r = rv[tid] - aj * qj[tid];
-          if (j > 0) r -= beta[j - 1] * V[(j - 1) * FNP + tid];
-          rv[tid] = r;
+        // start: warm Ritz vector (perturbed on a new outer iteration) or
+        // sqrt-weights times a fixed non-uniform pattern (sqrt-weights alone
+        // span the null vector: M W^1/2 1 = W^1/2 C w = 0)
+        double r0 = 0.0;
+        if (own && sw[tid] > 0.0) {
+          const double h = 0.5 + (tid * 0.6180339887498949 - floor(tid * 0.6180339887498949));
+          r0 = rs > 0 ? uv[tid] : (have_u ? uv[tid] + 1e-3 * sw[tid] * h : sw[tid] * h);
         }
-        if (tid == 0) alpha[j] = aj;
-        if (dbg && tid == 0 && rs == 0 && j == 0) { scal[10] = aj; scal[11] = rv[0]; scal[12] = yv[0]; scal[13] = xv[0]; }
+        const double nrm = sqrt(block_sum(r0 * r0, red));
+        if (own) {
+          const double q = r0 / nrm;
+          V[tid] = q;
+          xv[tid] = sw[tid] * q;
+        }
         __syncthreads();
-        // full reorthogonalisation (classical Gram-Schmidt, twice)
-        for (int pass = 0; pass < 2; ++pass) {
-          if (tid <= j) {
-            double h = 0.0;
-            for (int i = 0; i < FNP; ++i) h += V[tid * FNP + i] * rv[i];
-            svec[tid] = h;
-          }
-          __syncthreads();
-          if (tid < FNP) {
-            double r = rv[tid];
-            for (int q = 0; q <= j; ++q) r -= svec[q] * V[q * FNP + tid];
+        int m = 0;
+        bool done = false;
+        double tscale = 0.0;
+        double theta_lb = -1e300;   // top Ritz value of the previous check
+        int next_check = m_hint > 8 ? m_hint : 8;
+        for (int j = 0; j < msteps; ++j) {
+          // r = M q_j - a_j q_j - b_{j-1} q_{j-1}
+          if (dbg) t0c = clock64();
+          double r = cmul();
+          if (dbg) { const long long t = clock64(); tm[0] += t - t0c; t0c = t; }
+          const double qv = own ? V[j * VST + tid] : 0.0;
+          r = own ? sw[tid] * r : 0.0;
+          const double aj = block_sum(qv * r, red);
+          if (own) {
+            r -= aj * qv;
+            if (j > 0) r -= beta[j - 1] * V[(j - 1) * VST + tid];
             rv[tid] = r;
           }
+          if (tid == 0) alpha[j] = aj;
+          __syncthreads();
+          if (dbg) { const long long t = clock64(); tm[1] += t - t0c; t0c = t; }
+          // full re-orthogonalisation against q_0..q_j (classical GS, twice);
+          // dot products: 4 threads per basis vector, 32 entries each
+#pragma unroll 1
+          for (int pass = 0; pass < 2; ++pass) {
+            {
+              // 4 lanes per basis vector, entries interleaved (i = part + 4e)
+              const int qq = tid >> 2, part = tid & 3;
+              double h0 = 0.0, h1 = 0.0, h2 = 0.0, h3 = 0.0;
+              if (qq <= j) {
+                const double* vq = V + qq * VST + part;
+                const double* rp = rv + part;
+#pragma unroll
+                for (int e = 0; e < 128; e += 16) {
+                  h0 += vq[e] * rp[e];
+                  h1 += vq[e + 4] * rp[e + 4];
+                  h2 += vq[e + 8] * rp[e + 8];
+                  h3 += vq[e + 12] * rp[e + 12];
+                }
+              }
+              double h = (h0 + h1) + (h2 + h3);
+              h += dpp_f64<0xB1>(h);
+              h += dpp_f64<0x4E>(h);
+              if (part == 0 && qq <= j) hq[qq] = h;
+            }
+            __syncthreads();
+            if (own) {
+              double u0 = 0.0, u1 = 0.0, u2 = 0.0, u3 = 0.0;
+              int qq = 0;
+              for (; qq + 3 <= j; qq += 4) {
+                u0 += hq[qq] * V[qq * VST + tid];
+                u1 += hq[qq + 1] * V[(qq + 1) * VST + tid];
+                u2 += hq[qq + 2] * V[(qq + 2) * VST + tid];
+                u3 += hq[qq + 3] * V[(qq + 3) * VST + tid];
+              }
+              for (; qq <= j; ++qq) u0 += hq[qq] * V[qq * VST + tid];
+              r -= (u0 + u1) + (u2 + u3);
+              if (pass == 0) rv[tid] = r;
+            }
+            if (pass == 0) __syncthreads();
+          }
+          if (dbg) { const long long t = clock64(); tm[2] += t - t0c; t0c = t; }
+          const double bj = sqrt(block_sum(own ? r * r : 0.0, red));
+          if (dbg) { const long long t = clock64(); tm[3] += t - t0c; t0c = t; }
+          if (tid == 0) {
+            beta[j] = bj;
+            beta2[j] = bj * bj;
+          }
+          m = j + 1;
+          tscale = fmax(tscale, fabs(aj) + bj + (j > 0 ? beta[j - 1] : 0.0));
+          const bool breakdown = !(bj > 1e-14 * tscale);
+          const bool last = m == msteps || breakdown;
+          if (last || m >= next_check) {
+            __syncthreads();
+            // top eigenpair of T_m (wave 0, T in registers: lane q holds
+            // alpha_q, beta_q): multisection on Sturm counts, bracket from the
+            // previous check's Ritz value (interlacing: it only grows with m),
+            // then the eigenvector from a twisted factorisation
+            if (wave == 0) {
+              const double al = lane < m ? alpha[lane] : 0.0;
+              const double bl = lane + 1 < m ? beta[lane] : 0.0;
+              const double bp = (lane >= 1 && lane < m) ? beta[lane - 1] : 0.0;
+              const double b2l = bl * bl;
+              const double rad = fabs(bp) + fabs(bl);
+              double lo = wave_min(lane < m ? al - rad : 1e300);
+              double hi = wave_max(lane < m ? al + rad : -1e300);
+              if (theta_lb > lo && theta_lb < hi) lo = theta_lb;
+              const double tiny = 1e-300 + 1e-30 * tscale;
+              for (int round = 0; round < 16; ++round) {
+                const double x = lo + (hi - lo) * (lane + 1) / 65.0;
+                int cntb = 0;
+                double dd = readlane_f64(al, 0) - x;
+                if (fabs(dd) < tiny) dd = -tiny;
+                cntb += dd < 0.0;
+                for (int q = 1; q < m; ++q) {
+                  double rc = __builtin_amdgcn_rcp(dd);
+                  rc = rc * (2.0 - dd * rc);
+                  dd = (readlane_f64(al, q) - x) - readlane_f64(b2l, q - 1) * rc;
+                  if (fabs(dd) < tiny) dd = -tiny;
+                  cntb += dd < 0.0;
+                }
+                const unsigned long long ok = __builtin_amdgcn_ballot_w64(cntb >= m);
+                const int first = ok ? __builtin_ctzll(ok) : 64;
+                const double nlo = lo + (hi - lo) * first / 65.0;
+                const double nhi = first < 64 ? lo + (hi - lo) * (first + 1) / 65.0 : hi;
+                lo = nlo;
+                hi = nhi;
+                if (hi - lo <= 2e-16 * fmax(fabs(lo), fabs(hi))) break;
+              }
+              const double lm = 0.5 * (lo + hi);
+              // twisted factorisation of T - lm I: forward pivots dp, backward dm
+              double dpv = 0.0, dmv = 0.0;
+              {
+                double dp = readlane_f64(al, 0) - lm;
+                if (fabs(dp) < tiny) dp = -tiny;
+                dpv = writelane_f64(dp, 0, dpv);
+                for (int q = 1; q < m; ++q) {
+                  dp = (readlane_f64(al, q) - lm) - readlane_f64(b2l, q - 1) / dp;
+                  if (fabs(dp) < tiny) dp = -tiny;
+                  dpv = writelane_f64(dp, q, dpv);
+                }
+                double dm = readlane_f64(al, m - 1) - lm;
+                if (fabs(dm) < tiny) dm = -tiny;
+                dmv = writelane_f64(dm, m - 1, dmv);
+                for (int q = m - 2; q >= 0; --q) {
+                  dm = (readlane_f64(al, q) - lm) - readlane_f64(b2l, q) / dm;
+                  if (fabs(dm) < tiny) dm = -tiny;
+                  dmv = writelane_f64(dm, q, dmv);
+                }
+              }
+              // twist index: smallest |gamma_q| = |dp_q + dm_q - (alpha_q - lm)|
+              double gam = lane < m ? fabs(dpv + dmv - (al - lm)) : 1e308;
+              int tw = lane;
+#pragma unroll
+              for (int off = 32; off >= 1; off >>= 1) {
+                const double og = __shfl_xor(gam, off);
+                const int ot = __shfl_xor(tw, off);
+                if (og < gam || (og == gam && ot < tw)) {
+                  gam = og;
+                  tw = ot;
+                }
+              }
+              tw = __builtin_amdgcn_readfirstlane(tw);
+              // z_tw = 1; z_q = -(b_q / dp_q) z_{q+1} below, z_{q+1} = -(b_q / dm_{q+1}) z_q above
+              const double dmn = __shfl_down(dmv, 1);
+              const double fdown = lane < m ? -bl / dpv : 0.0;
+              const double fup = lane + 1 < m ? -bl / dmn : 0.0;
+              double zv = lane == tw ? 1.0 : 0.0;
+              double z = 1.0;
+              for (int q = tw - 1; q >= 0; --q) {
+                z *= readlane_f64(fdown, q);
+                zv = writelane_f64(z, q, zv);
+              }
+              z = 1.0;
+              for (int q = tw; q + 1 < m; ++q) {
+                z *= readlane_f64(fup, q);
+                zv = writelane_f64(z, q + 1, zv);
+              }
+              if (lane >= m) zv = 0.0;
+              const double amax = wave_max(fabs(zv));
+              const double zs = zv / amax;
+              const double nn = amax * sqrt(wave_sum(zs * zs));
+              zv = zv / nn;
+              if (lane < m) svec[lane] = zv;
+              if (lane == 0) {
+                scal[1] = lm;
+                scal[2] = fabs(bj * readlane_f64(zv, m - 1));
+              }
+            }
+            __syncthreads();
+            lam = scal[1];
+            resid_last = scal[2];
+            theta_lb = lam;
+            next_check = m + 8;
+            if (dbg) { const long long t = clock64(); tm[4] += t - t0c; t0c = t; }
+            done = last || resid_last <= 1e-13 * fabs(lam);
+            if (done) break;
+          }
+          if (own) {
+            const double qn = r / bj;
+            V[(j + 1) * VST + tid] = qn;
+            xv[tid] = sw[tid] * qn;
+          }
           __syncthreads();
         }
-        const double bj = sqrt(block_sum(tid < FNP ? rv[tid] * rv[tid] : 0.0, red));
-        if (tid == 0) beta[j] = bj;
-        if (dbg && tid == 0 && rs == 0 && j == 0) { scal[14] = bj; scal[15] = V[0]; }
+        // Ritz vector
+        if (own) {
+          double u = 0.0;
+          for (int q = 0; q < m; ++q) u += V[q * VST + tid] * svec[q];
+          uv[tid] = u;
+        }
+        m_last = m;
+        rs_used = rs + 1;
+        m_hint = m;
         __syncthreads();
-        if (j + 1 >= msteps || !(bj > 1e-300) || bj <= 1e-13 * (aj > 0 ? aj : -aj)) {
-          mused = j + 1;
-          break;
-        }
-        if (tid < FNP) V[(j + 1) * FNP + tid] = rv[tid] / bj;
-        __syncthreads();
-      }
-      // ---- top eigenpair of the tridiagonal (alpha, beta[0..m-2]) ----
-      if (wave == 0) {
-        // Gershgorin bounds
-        double lo = 1e300, hi = -1e300;
-        for (int q = 0; q < mused; ++q) {
-          const double rad = (q > 0 ? fabs(beta[q - 1]) : 0.0) + (q + 1 < mused ? fabs(beta[q]) : 0.0);
-          lo = fmin(lo, alpha[q] - rad);
-          hi = fmax(hi, alpha[q] + rad);
-        }
-        // multisection for the largest eigenvalue: count(x) = #eig < x;
-        // the largest lies where count crosses from mused-1 to mused
-        for (int round = 0; round < 12; ++round) {
-          const double x = lo + (hi - lo) * (lane + 1) / 65.0;
-          const int cnt = sturm_count(alpha, beta, mused, x);
-          const unsigned long long ok = __builtin_amdgcn_ballot_w64(cnt >= mused);  // x above all
-          // first lane whose x is above the top eigenvalue
-          const int first = ok ? __builtin_ctzll(ok) : 64;
-          const double nlo = lo + (hi - lo) * first / 65.0;
-          const double nhi = first < 64 ? lo + (hi - lo) * (first + 1) / 65.0 : hi;
-          lo = nlo;
-          hi = nhi;
-        }
-        const double lam = 0.5 * (lo + hi);
-        if (lane == 0) {
-          scal[1] = lam;
-          // inverse iteration on (T - lam I) with a tiny shift
-          const int m = mused;
-          double shift = lam + 1e-12 * (fabs(lam) + 1e-300);
-          for (int q = 0; q < m; ++q) svec[q] = 1.0;
-          for (int pass = 0; pass < 3; ++pass) {
-            // Thomas algorithm on (T - shift I) x = svec
-            double* cp = tcp;
-            double* dp = tdp;
-            double den = alpha[0] - shift;
-            if (den == 0.0) den = 1e-300;
-            cp[0] = (m > 1 ? beta[0] : 0.0) / den;
-            dp[0] = svec[0] / den;
-            for (int q = 1; q < m; ++q) {
-              den = (alpha[q] - shift) - beta[q - 1] * cp[q - 1];
-              if (den == 0.0) den = 1e-300;
-              cp[q] = (q + 1 < m ? beta[q] : 0.0) / den;
-              dp[q] = (svec[q] - beta[q - 1] * dp[q - 1]) / den;
-            }
-            svec[m - 1] = dp[m - 1];
-            for (int q = m - 2; q >= 0; --q) svec[q] = dp[q] - cp[q] * svec[q + 1];
-            double nn = 0.0;
-            for (int q = 0; q < m; ++q) nn += svec[q] * svec[q];
-            nn = sqrt(nn);
-            for (int q = 0; q < m; ++q) svec[q] /= nn;
-          }
-          iscal[1] = m;
-        }
-      }
-      __syncthreads();
-      lam = scal[1];
-      const int m = iscal[1];
-      if (tid < FNP) {
-        double u = 0.0;
-        for (int q = 0; q < m; ++q) u += V[q * FNP + tid] * svec[q];
-        uv[tid] = u;
-      }
-      __syncthreads();
-      // Ritz residual |beta_m s_m|: stop when the pair is converged to fp64
-      // level or the Krylov space is the whole active subspace
-      const double resid = fabs(beta[m - 1] * svec[m - 1]);
-      resid_last = resid;
-      m_last = m;
-      rs_used = rs + 1;
-      if (m >= nact || resid <= 1e-13 * fabs(lam)) break;
-      __syncthreads();
+        if (m >= nact || resid_last <= 1e-13 * fabs(lam)) break;
       }
       have_u = true;
       if (dbg && it < 256) {
         double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
-        if (tid < FNP) rec[tid] = c[tid];
+        if (own) rec[tid] = c[tid];
         if (tid == 0) {
           rec[FNP] = lam;
           rec[FNP + 1] = m_last;
           rec[FNP + 2] = resid_last;
           rec[FNP + 3] = rs_used;
-          for (int q = 4; q < 16; ++q) rec[FNP + q] = scal[q];
+          rec[FNP + 4] = nact;
+          rec[FNP + 5] = scal[0];
+          for (int q = 0; q < 5; ++q) rec[FNP + 6 + q] = static_cast<double>(tm[q]);
         }
       }
-      // ---- early exit ----
+      // ---- early exit (robust_estimator.py:164 / :70) ----
       if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
-      // ---- tau = (C W^1/2 u)^2 / lam ----
-      cop(uv, rv, false);
-      if (tid < FNP) tau[tid] = active[tid] ? rv[tid] * rv[tid] / lam : -1.0;
+      // ---- tau_j = ((x_j - mu).v)^2 = (C W^1/2 u)_j^2 / lam ----
+      if (own) xv[tid] = sw[tid] * uv[tid];
       __syncthreads();
+      const double cu = cmul();
+      const double ti = own ? cu * cu / lam : 0.0;
       if constexpr (MODE == 0) {
-        if (tid == 0) {
-          int best = -1;
-          double bv = 0.0;
-          for (int i = 0; i < n; ++i)
-            if (active[i] && (best < 0 || tau[i] > bv)) { bv = tau[i]; best = i; }
-          iscal[2] = best;
-          scal[2] = bv;
+        // c *= 1 - tau/tau_max; drop argmax (first index); c /= |c|_1
+        double tmax = 0.0;
+        const int p = block_argmax_first(own && active[tid] ? ti : -__builtin_inf(), tid, red,
+                                         reinterpret_cast<int*>(iscal), &tmax);
+        double cn = 0.0;
+        if (own && active[tid] && tid != p) cn = c[tid] * (1.0 - ti / tmax);
+        const double l1 = block_sum(fabs(cn), red);
+        if (own) {
+          c[tid] = cn / l1;
+          if (tid == p) active[tid] = 0;
         }
-        __syncthreads();
-        const int p = iscal[2];
-        const double tmax = scal[2];
-        if (tid < FNP && active[tid]) c[tid] = c[tid] * (1.0 - tau[tid] / tmax);
-        __syncthreads();
-        if (tid == 0 && p >= 0) {
-          active[p] = 0;
-          c[p] = 0.0;
-        }
-        __syncthreads();
-        const double l1 = block_sum(tid < FNP && active[tid] ? fabs(c[tid]) : 0.0, red);
-        if (tid < FNP && active[tid]) c[tid] = c[tid] / l1;
         __syncthreads();
       } else {
-        if (tid < FNP && active[tid]) c[tid] = c[tid] * (1.0 - step * tau[tid]);
+        // c *= 1 - step*tau, then the KL projection onto
+        // {sum c = 1, c <= cap} (robust_estimator.py:77-99)
+        const int nk = n_keep;
+        const double cap = 1.0 / (1.0 - A.eps) / nk;
+        if (own && active[tid]) c[tid] = c[tid] * (1.0 - step * ti);
         __syncthreads();
-        // ---- KL projection onto {sum c = 1, c <= cap} (robust_estimator.py:77-99) ----
-        // compact kept weights in client order: cc[0..nk)
-        double* cc = rv;        // compacted c
-        double* cand = yv;      // candidate KL per i (thread i)
-        int* desc = reinterpret_cast<int*>(xv);   // ranks: desc[q] = compact index of q-th largest
-        int* rank = desc + FNP;                   // rank of compact index
-        if (tid == 0) {
-          int q = 0;
-          for (int i = 0; i < n; ++i)
-            if (active[i]) cc[q++] = c[i];
-          // descending order = np.flip(np.argsort(c)) ; insertion sort by value,
-          // ties: later index first (flip of a stable ascending order)
-          for (int a = 0; a < q; ++a) desc[a] = a;
-          for (int a = 1; a < q; ++a) {
-            const int v = desc[a];
-            int b = a - 1;
-            while (b >= 0 && (cc[desc[b]] < cc[v] || (cc[desc[b]] == cc[v] && desc[b] < v))) {
-              desc[b + 1] = desc[b];
-              --b;
-            }
-            desc[b + 1] = v;
-          }
-          for (int a = 0; a < q; ++a) rank[desc[a]] = a;
-          iscal[3] = q;
+        double* cc = rv;   // compacted weights
+        if (tid < nk) cc[tid] = c[kidx[tid]];
+        __syncthreads();
+        // descending rank; ties: later compact index first (flip of a
+        // stable ascending order)
+        if (tid < nk) {
+          const double v = cc[tid];
+          int rk = 0;
+          for (int q = 0; q < nk; ++q) rk += (cc[q] > v || (cc[q] == v && q > tid)) ? 1 : 0;
+          irank[tid] = rk;
+          sv[rk] = v;
+          hl[rk] = v * log(v / cap);
         }
         __syncthreads();
-        const int nk = iscal[3];
-        const double cap = 1.0 / (1.0 - A.eps) / nk;
-        // candidate i (thread i): cap the i+1 largest, rescale the rest
-        double kl = __builtin_inf();
-        int feasible = 0, stop = 0;
+        // candidate i caps the i+1 largest at cap and rescales the rest
+        double negkl = -__builtin_inf(), scale = 0.0;
+        int stop = 1 << 30;
         if (tid < nk) {
           const int i = tid;
           const double clip = 1.0 - np_pw64(0, i + 1, [&](int) { return cap; });
           if (clip <= 0.0) {
-            stop = 1;
+            stop = i;
           } else if (i + 1 < nk) {
-            const double norm = np_pw64(0, nk - i - 1, [&](int q) { return cc[desc[i + 1 + q]]; });
-            const double scale = clip / norm;
-            if (!(cc[desc[i + 1]] * scale > cap)) {
-              feasible = 1;
-              kl = np_pw64(0, nk, [&](int q) {
-                const double x = cc[q];
-                const double y = rank[q] <= i ? cap : cc[q] * scale;
-                return (x > 0.0 && y > 0.0) ? x * log(x / y) : (x == 0.0 && y >= 0.0 ? 0.0 : __builtin_inf());
-              });
+            const double norm = np_pw64(i + 1, nk - i - 1, [&](int q) { return sv[q]; });
+            scale = clip / norm;
+            if (!(sv[i + 1] * scale > cap)) {
+              double head = 0.0;
+              for (int q = 0; q <= i; ++q) head += hl[q];
+              negkl = -(head - norm * log(scale));
             }
           }
         }
-        __syncthreads();
-        if (tid < nk) {
-          cand[tid] = feasible ? kl : __builtin_inf();
-          reinterpret_cast<int*>(tau)[tid] = stop;   // reuse tau storage for flags
+        const int istop = block_min_int(stop, reinterpret_cast<int*>(iscal));
+        if (tid >= istop) negkl = -__builtin_inf();
+        double best = 0.0;
+        const int bi = block_argmax_first(negkl, tid, red, reinterpret_cast<int*>(iscal), &best);
+        if (!(best > -__builtin_inf())) {
+          if (tid == 0) *A.status = 2;   // projected_c None -> TypeError in the reference
+          break;
         }
+        if (tid == bi) scal[3] = scale;
         __syncthreads();
-        if (tid == 0) {
-          // the reference loops i upward and breaks at the first clip <= 0
-          int best = -1;
-          double bv = 0.0;
-          for (int i = 0; i < nk; ++i) {
-            if (reinterpret_cast<int*>(tau)[i]) break;
-            if (cand[i] < __builtin_inf() && (best < 0 || cand[i] < bv)) { bv = cand[i]; best = i; }
-          }
-          iscal[4] = best;
-          if (best < 0) *A.status = 2;   // projected_c None -> TypeError in the reference
-        }
+        if (tid < nk) c[kidx[tid]] = irank[tid] <= bi ? cap : cc[tid] * scal[3];
         __syncthreads();
-        const int bi = iscal[4];
-        if (bi >= 0) {
-          // apply the chosen candidate (per compact index)
-          const double clip = 1.0 - np_pw64(0, bi + 1, [&](int) { return cap; });
-          const double norm = np_pw64(0, nk - bi - 1, [&](int q) { return cc[desc[bi + 1 + q]]; });
-          const double scale = clip / norm;
-          if (tid == 0) {
-            int q = 0;
-            for (int i2 = 0; i2 < n; ++i2)
-              if (active[i2]) {
-                c[i2] = rank[q] <= bi ? cap : cc[q] * scale;
-                ++q;
-              }
-          }
-        }
-        __syncthreads();
-        if (bi < 0) break;
       }
     }
 
     // ================= Phase D: weighted mean over the chunk ================
     {
-      double cs = 0.0;
       if (tid == 0) {
-        // np.average's scale: pairwise sum of the (kept) weights in order
+        // np.average's scale: pairwise sum of the kept weights in order
         int q = 0;
         for (int i = 0; i < n; ++i)
           if (active[i]) rv[q++] = c[i];
-        cs = np_pw64(0, q, [&](int z) { return rv[z]; });
-        scal[3] = cs;
+        scal[4] = np_pw64(0, q, [&](int z) { return rv[z]; });
       }
       __syncthreads();
-      cs = scal[3];
+      const double cs = scal[4];
       for (int cc2 = tid; cc2 < k; cc2 += 256) {
         double s = 0.0;
         for (int i = 0; i < n; ++i)
@@ -700,7 +871,7 @@ __global__ void __launch_bounds__(256) spectral_filter_kernel(FilterArgs A) {
 }
 
 size_t filter_lds_bytes() {
-  return FilterShared::kUnionBytes + sizeof(double) * (9 * FNP + 5 * LMAX + 8 + 16) + sizeof(int) * (FNP + 16) + 64;
+  return FilterShared::kUnionBytes + sizeof(double) * (9 * FNP + 6 * LMAX + 32) + sizeof(int) * (3 * FNP + 16);
 }
 
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,

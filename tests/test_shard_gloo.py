@@ -1,0 +1,151 @@
+"""world_size-2 gloo tests of the d-sharding layer (srfl_amd/shard.py) on CPU.
+
+The per-shard operations are the oracle's numpy restatements (the GPU ranks
+pass the HIP entry points instead, shard.engine_ops()); what is tested here is
+the sharding itself: balanced chunk-aligned bounds, the all-gather assembly,
+filters restarting their chunking exactly where the unsharded path does, and
+Krum from an all-reduced partial centred Gram."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _setup_paths():
+    for p in (ROOT, HERE, os.path.join(HERE, "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import srfl_loader
+    srfl_loader.load()
+
+
+def _centred_gram(x):
+    z = x.astype(np.float64) - x.astype(np.float64).mean(axis=0)
+    return z @ z.T
+
+
+def _worker(rank, world, port, results):
+    _setup_paths()
+    from srfl_amd import shard
+    from oracle import robust_np as orc
+    from synth import make_rows
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        # coordinate-wise: trimmed mean / median over a ragged d
+        n, d = 37, 1001
+        x = make_rows(n, d, seed=11, byz=5)
+        lo, hi = shard.shard_bounds(d, world, rank)
+        Xs = torch.from_numpy(np.ascontiguousarray(x[:, lo:hi]))
+        tm = shard.coordinatewise(lambda X: torch.from_numpy(np.asarray(orc.trimmed_mean(list(X.numpy())))),
+                                  Xs, d)
+        md = shard.coordinatewise(lambda X: torch.from_numpy(np.asarray(orc.median(list(X.numpy())))), Xs, d)
+        out["trimmed"] = tm.numpy()
+        out["median"] = md.numpy()
+        # chunked filter: shards aligned to itv
+        itv = 40
+        xf = make_rows(24, 230, seed=12, byz=4)
+        lo, hi = shard.shard_bounds(230, world, rank, align=shard.filter_align(itv))
+        Xf = torch.from_numpy(np.ascontiguousarray(xf[:, lo:hi]))
+        fl = shard.coordinatewise(lambda X: torch.from_numpy(orc.filterL2(list(X.numpy()), 0.2, 0.02, 20, itv)),
+                                  Xf, 230, align=itv)
+        out["filter"] = fl.numpy()
+        # Krum from the all-reduced partial Gram
+        xk = make_rows(30, 777, seed=13, byz=6)
+        lo, hi = shard.shard_bounds(777, world, rank)
+        Xk = torch.from_numpy(np.ascontiguousarray(xk[:, lo:hi]))
+
+        def select(G, f):
+            g = G.numpy()
+            sq = np.diag(g)[:, None] + np.diag(g)[None, :] - 2 * g
+            dd = np.sqrt(np.maximum(sq, 0)).astype(np.float32)
+            return int(np.argmin(orc.krum_scores_from_dist(dd, f)))
+
+        row, idx = shard.krum(lambda X: torch.from_numpy(_centred_gram(X.numpy())), select, Xk, 777, 6)
+        out["krum_row"] = row.numpy()
+        out["krum_idx"] = idx
+        results[rank] = out
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def two_rank_results():
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    results = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, results)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+        assert p.exitcode == 0, "gloo worker failed"
+    return dict(results)
+
+
+def test_shard_bounds_cover_and_align():
+    _setup_paths()
+    from srfl_amd import shard
+    for d in (1, 7, 1000, 1001, 12345):
+        for world in (1, 2, 3, 8):
+            for align in (1, 64, 1000):
+                b = shard.all_bounds(d, world, align)
+                assert b[0][0] == 0 and b[-1][1] == d
+                for (l0, h0), (l1, h1) in zip(b, b[1:]):
+                    assert h0 == l1
+                for lo, hi in b:
+                    assert lo % align == 0 or lo == d
+                widths = [hi - lo for lo, hi in b]
+                assert max(widths) - min(widths) <= align
+
+
+def test_sharded_coordinatewise_equals_unsharded(two_rank_results):
+    _setup_paths()
+    from oracle import robust_np as orc
+    from synth import make_rows
+    x = make_rows(37, 1001, seed=11, byz=5)
+    for r in (0, 1):
+        np.testing.assert_array_equal(two_rank_results[r]["trimmed"], orc.trimmed_mean(list(x)))
+        np.testing.assert_array_equal(two_rank_results[r]["median"], orc.median(list(x)))
+
+
+def test_sharded_filter_equals_unsharded(two_rank_results):
+    _setup_paths()
+    from oracle import robust_np as orc
+    from synth import make_rows
+    xf = make_rows(24, 230, seed=12, byz=4)
+    want = orc.filterL2(list(xf), 0.2, 0.02, 20, 40)
+    for r in (0, 1):
+        np.testing.assert_allclose(two_rank_results[r]["filter"], want, rtol=1e-12, atol=1e-15)
+
+
+def test_sharded_krum_equals_unsharded(two_rank_results):
+    _setup_paths()
+    from oracle import robust_np as orc
+    from synth import make_rows
+    xk = make_rows(30, 777, seed=13, byz=6)
+    row, idx = orc.krum(list(xk), 6)
+    for r in (0, 1):
+        assert two_rank_results[r]["krum_idx"] == idx
+        np.testing.assert_array_equal(two_rank_results[r]["krum_row"], row)

@@ -35,3 +35,28 @@ for it in range(recs.shape[0]):
     print("    scal4..15", r[132:144])
 print("out", out.cpu().numpy()[:8])
 print("want", z["out"].ravel()[:8] if "out" in z else None)
+
+if len(sys.argv) > 2 and sys.argv[2] == "synthetic":
+    for mode in (0, 1):
+        g = torch.Generator(device="cuda").manual_seed(1)
+        Y = 0.01 * torch.randn(128, 1000, device="cuda", generator=g)
+        out, G, recs = engine.filter_debug(Y, mode, 0.2, 1e-5, 20, 1000)
+        ms, rss = [], []
+        for it in range(recs.shape[0]):
+            r = recs[it].numpy()
+            if np.isnan(r[128]):
+                break
+            ms.append(int(r[129]))
+            rss.append(int(r[131]))
+        print("mode", mode, "iters", len(ms), "steps", ms, "restarts", rss)
+        print("   resid", [float("%.1e" % recs[i, 130]) for i in range(len(ms))][:10])
+        tsum = recs[:len(ms), 134:139].numpy().sum(0)
+        print("   cycles cmul/aj/reorth/beta/check per step:", (tsum / max(1, sum(ms))).round(0), "total Mcyc", tsum.sum() / 1e6)
+        torch.cuda.synchronize()
+        import time
+        t0 = time.perf_counter()
+        for _ in range(3):
+            engine.filter_l2(Y, 0.2, 1e-5, 20, 1000, check=False) if mode == 0 else \
+                engine.ex_noregret(Y, 0.2, 1e-5, 20, 1000, check=False)
+        torch.cuda.synchronize()
+        print("   one chunk: %.3f ms" % ((time.perf_counter() - t0) / 3 * 1e3))
