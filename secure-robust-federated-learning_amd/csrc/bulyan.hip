@@ -56,19 +56,39 @@ __global__ void __launch_bounds__(256) select_rows_kernel(const float* __restric
   const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
   const unsigned off = (t < last ? t : last) * 4u;
   const int k_bottom = MODE == 0 ? (P - n) / 2 : 0;
+  // the row list in VGPRs (lane l holds rows[l], rows[64 + l], ...): each
+  // row index is then a readlane, not a dependent scalar load per row
+  constexpr int RW = (P + 63) / 64;
+  int rl[RW];
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int li = 64 * q + static_cast<int>(t & 63);
+    rl[q] = rows[li < n ? li : n - 1];
+  }
+  constexpr int kFirstPad = P > 16 ? P - 16 : 0;   // rows below this are always real (n > P - 16)
   float v[P2];
 #pragma unroll
-  for (int i = 0; i < P; ++i) {
-    const int r = i < n ? i : n - 1;
-    const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(rows[r]) * ldx + base));
+  for (int i = 0; i < kFirstPad; ++i) {
+    // lane i % 64 of block i / 64 holds rows[i]
+    const int row = __builtin_amdgcn_readlane(rl[i / 64], i % 64);
+    const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
+    v[i] = ld_lane(rp, off);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = kFirstPad; i < P; ++i) {
+    // lane i % 64 of block i / 64 holds rows[min(i, n - 1)] (clamped above)
+    const int row = __builtin_amdgcn_readlane(rl[i / 64], i % 64);
+    const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
     const float x = ld_lane(rp, off);
     __builtin_amdgcn_sched_barrier(0);
     const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
     v[i] = i < n ? x : pad;
   }
+  // NaN detection over all slots (pads are +-inf, never NaN)
   float m = v[0];
 #pragma unroll
-  for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, (i < n) ? v[i] : v[0]);
+  for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, v[i]);
   int nan_cnt = 0;
   if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
 #pragma unroll
@@ -84,10 +104,14 @@ __global__ void __launch_bounds__(256) select_rows_kernel(const float* __restric
     res = (n & 1) ? v[P / 2 - 1] : (v[P / 2 - 1] + v[P / 2]) * 0.5f;
     if (nan_cnt > 0) res = qnan();
   } else {
-    network_fast<P2, P, 0, P>(v);
+    // lo = int(0.1 n), hi = n - lo over n in (P-16, P]: the kept window is
+    // always inside [int(0.1 (P-15)), P - int(0.1 P)) -> prune the cone to it
+    constexpr int OLO = (P > 16 ? P - 15 : 1) / 10;
+    constexpr int OHI = P - P / 10;
+    network_fast<P2, P, OLO, OHI>(v);
     float acc = 0.f;
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
+    for (int p = OLO; p < OHI; ++p) {
       if (p >= lo && p < hi) {
         asm volatile("");
         acc += v[p];
@@ -106,6 +130,7 @@ __global__ void __launch_bounds__(256) select_rows_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 constexpr int kDistChunks = 128;
 
+template <bool VEC>  // VEC: rows and agg 16-byte aligned and chunk % 4 == 0
 __global__ void __launch_bounds__(256) row_dist_partial_kernel(const float* __restrict__ X, int64_t ldx,
                                                                const int* __restrict__ rows, int64_t d,
                                                                const float* __restrict__ agg, int64_t chunk,
@@ -116,9 +141,43 @@ __global__ void __launch_bounds__(256) row_dist_partial_kernel(const float* __re
   const int64_t j0 = static_cast<int64_t>(c) * chunk;
   const int64_t j1 = j0 + chunk < d ? j0 + chunk : d;
   float s = 0.f;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
-    const float df = agg[j] - x[j];
-    s = __builtin_fmaf(df, df, s);
+  if constexpr (VEC) {
+    // 4 independent float4 loads per thread in flight (16 KB per block step)
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t j = j0 + 4 * threadIdx.x;
+    for (; j + 3 * 1024 + 3 < j1; j += 4 * 1024) {
+      f32x4 xa[4], aa[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xa[u] = *reinterpret_cast<const f32x4*>(x + j + 1024 * u);
+        aa[u] = *reinterpret_cast<const f32x4*>(agg + j + 1024 * u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 df = aa[u] - xa[u];
+        s0 = __builtin_fmaf(df[0], df[0], s0);
+        s1 = __builtin_fmaf(df[1], df[1], s1);
+        s2 = __builtin_fmaf(df[2], df[2], s2);
+        s3 = __builtin_fmaf(df[3], df[3], s3);
+      }
+    }
+    for (; j + 3 < j1; j += 1024) {
+      const f32x4 df = *reinterpret_cast<const f32x4*>(agg + j) - *reinterpret_cast<const f32x4*>(x + j);
+      s0 = __builtin_fmaf(df[0], df[0], s0);
+      s1 = __builtin_fmaf(df[1], df[1], s1);
+      s2 = __builtin_fmaf(df[2], df[2], s2);
+      s3 = __builtin_fmaf(df[3], df[3], s3);
+    }
+    for (int64_t q = j; q < j1 && q < j + 4; ++q) {   // ragged tail of the chunk
+      const float df = agg[q] - x[q];
+      s0 = __builtin_fmaf(df, df, s0);
+    }
+    s = (s0 + s1) + (s2 + s3);
+  } else {
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+      const float df = agg[j] - x[j];
+      s = __builtin_fmaf(df, df, s);
+    }
   }
   // block reduce (fixed order)
   __shared__ float red[256];
@@ -365,8 +424,9 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   hipLaunchKernelGGL(iota_kernel, dim3(cdiv(theta, 256)), dim3(256), 0, s, order, theta);
   rc = launch_status("iota_kernel");
   if (rc) return rc;
-  const int64_t chunk = cdiv(d, kDistChunks);
+  const int64_t chunk = cdiv(cdiv(d, kDistChunks), 4) * 4;
   const int nchunks = static_cast<int>(cdiv(d, chunk));
+  const bool dist_vec = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && (ldx % 4 == 0) && (d % 4 == 0);
   int* cur = rows_a;
   int* nxt = rows_b;
   for (int t = 0; t < theta; ++t) {
@@ -380,8 +440,12 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
       rc = launch_select_rows<1>(X, ldx, cur, nr, d, lo, hi, agg, s);
     }
     if (rc) return rc;
-    hipLaunchKernelGGL(row_dist_partial_kernel, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg, chunk,
-                       partial);
+    if (dist_vec)
+      hipLaunchKernelGGL(row_dist_partial_kernel<true>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg,
+                         chunk, partial);
+    else
+      hipLaunchKernelGGL(row_dist_partial_kernel<false>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg,
+                         chunk, partial);
     rc = launch_status("row_dist_partial_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, partial, cur, nr, nchunks, nxt, status);

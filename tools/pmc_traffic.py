@@ -1,0 +1,90 @@
+"""Collect a profiling session (tools/profile_round.sh) into profiles/.
+
+For every workload: copies the rocprofv3 kernel stats CSV to
+profiles/<tag>_<workload>_kernel_stats.csv; for the PMC workloads computes
+the per-launch HBM bytes of the dominant kernel,
+    traffic = 2 * FETCH_SIZE + WRITE_SIZE   (bytes; FETCH_SIZE is reported in
+    KiB and counts half the bytes of wide coalesced reads on gfx950,
+    MI355X_MICROARCH.md HBM/rocprofv3 section),
+and merges it into profiles/traffic.json under "agg:N=<n>:d=<d>".
+
+Usage: python tools/pmc_traffic.py gpurun_out/prof_r01 [tag]
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DOMINANT = {"trimmedmean": "select_reg_kernel", "median": "select_reg_kernel", "average": "average",
+            "trimmedmean_n100": "select_reg_kernel", "krum": "gram_partial_kernel"}
+
+
+def _find(d, pat):
+    hits = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    return hits[0] if hits else None
+
+
+def bench_line(logf):
+    for ln in open(logf):
+        if ln.startswith("{"):
+            return json.loads(ln)
+    return None
+
+
+def pmc_mean(d, kernel_sub):
+    f = _find(d, "*counter_collection.csv")
+    if not f:
+        return None, None
+    vals, name = [], None
+    for r in csv.DictReader(open(f)):
+        if kernel_sub in r["Kernel_Name"]:
+            vals.append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"]
+    return (sum(vals) / len(vals) if vals else None), name
+
+
+def main():
+    src = sys.argv[1]
+    tag = sys.argv[2] if len(sys.argv) > 2 else os.path.basename(src.rstrip("/"))
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    for logf in sorted(glob.glob(os.path.join(src, "*.log"))):
+        name = os.path.basename(logf)[:-4]
+        if name.startswith("pmc_"):
+            continue
+        st = _find(os.path.join(src, name), "*kernel_stats.csv")
+        if st:
+            shutil.copy(st, os.path.join(prof, "%s_%s_kernel_stats.csv" % (tag, name)))
+        line = bench_line(logf)
+        if line:
+            with open(os.path.join(prof, "%s_%s_bench.json" % (tag, name)), "w") as fh:
+                json.dump(line, fh, indent=1)
+    tj_path = os.path.join(prof, "traffic.json")
+    tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
+    for d in sorted(glob.glob(os.path.join(src, "pmc_*_FETCH_SIZE"))):
+        name = re.match(r"pmc_(.*)_FETCH_SIZE", os.path.basename(d)).group(1)
+        sub = DOMINANT.get(name, "sra::")
+        fetch_kib, kname = pmc_mean(d, sub)
+        write_kib, _ = pmc_mean(os.path.join(src, "pmc_%s_WRITE_SIZE" % name), sub)
+        line = bench_line(os.path.join(src, "%s.log" % name))
+        if fetch_kib is None or write_kib is None or line is None:
+            continue
+        cfg = line["config"]
+        key = "%s:N=%d:d=%d" % (cfg["aggregator"], cfg["clients"], cfg["d_per_gpu"])
+        traffic = 2 * fetch_kib * 1024 + write_kib * 1024
+        tj[key] = {"kernel": kname, "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
+                   "hbm_bytes_per_launch": traffic,
+                   "algorithmic_bytes_per_launch": line["roofline"].get("algorithmic_bytes_per_launch"),
+                   "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of wide reads)",
+                   "source": tag}
+        print(key, "traffic %.4g B/launch" % traffic)
+    with open(tj_path, "w") as fh:
+        json.dump(tj, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round profiling session (run on the GPU box from the repo root):
+#   kernel-trace --stats of bench.py per workload, then FETCH_SIZE / WRITE_SIZE
+#   passes (each its own rocprofv3 run, --kernel-trace only) for the HBM-bound
+#   kernels.  Outputs under gpurun_out/$TAG/.  Stops at the first failure.
+set -u
+TAG=${TAG:-prof_r01}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUTD="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUTD"
+cd /tmp && export TMPDIR=/tmp
+WORKLOADS=${WORKLOADS:-"trimmedmean|--agg trimmedmean
+median|--agg median
+average|--agg average
+trimmedmean_n100|--agg trimmedmean --clients 100
+krum|--agg krum --d 1e7
+bulyankrum|--agg bulyankrum --d 1e7
+bulyantrimmedmean|--agg bulyantrimmedmean --d 1e7 --steps 2
+filterl2|--agg filterl2 --d 1e7 --steps 2
+ex_noregret|--agg ex_noregret --d 1e7 --steps 2"}
+PMC_WORKLOADS=${PMC_WORKLOADS:-"trimmedmean median average krum"}
+while IFS='|' read -r name args; do
+  [[ -z "$name" ]] && continue
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUTD/$name" -o run \
+    -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-host $args > "$OUTD/$name.log" 2>&1 \
+    || { echo "trace $name failed rc=$?"; exit 1; }
+  echo "trace $name ok"
+done <<< "$WORKLOADS"
+for name in $PMC_WORKLOADS; do
+  args=$(printf '%s\n' "$WORKLOADS" | awk -F'|' -v n="$name" '$1==n{print $2}')
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d "$OUTD/pmc_${name}_$ctr" -o run \
+      -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-host $args > "$OUTD/pmc_${name}_$ctr.log" 2>&1 \
+      || { echo "pmc $name $ctr failed rc=$?"; exit 1; }
+    echo "pmc $name $ctr ok"
+  done
+done
+echo done
