@@ -164,6 +164,47 @@ int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int3
                          double eps, double sigma, double expansion, double* out, int32_t* status, double* dbg,
                          void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Cross-layer-norm clipping (k7): the stateful inline aggregators           */
+/* iclr2022_bucketing (src/simulate.py:335-366) and icml2021_history (:367-388) */
+/* ------------------------------------------------------------------------ */
+
+/* out[w, :] = mean of X rows [w*stride, min(w*stride + width, n)) for w < nwin:
+ * sequential sum over the window's rows in the input precision, divided by the
+ * row count (an empty window gives NaN, like np.average of an empty list).
+ * stride = 1, width = perround // buckets are the overlapping windows
+ * choices[b : b + perround//buckets] of src/simulate.py:344-351. */
+int sra_window_mean_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t stride, int32_t width,
+                        int32_t nwin, float* out, int64_t ldo, void* stream);
+int sra_window_mean_f64(const double* X, int64_t n, int64_t d, int64_t ldx, int32_t stride, int32_t width,
+                        int32_t nwin, double* out, int64_t ldo, void* stream);
+
+/* Workspace for sra_clip_scale_*, in bytes (seg: host array of nseg+1 offsets). */
+int sra_clip_workspace_bytes(int64_t k, const int64_t* seg, int32_t nseg, size_t* bytes);
+
+/* Per-row clipping factor against prev (d fp64, device) with the norm taken
+ * across all layer segments: sq_r = sum_l ||M[r, seg_l] - prev[seg_l]||^2 (each
+ * layer norm squared after the sqrt, in layer order), norm_r = sqrt(sq_r),
+ * scale[r] = min(1, tau / norm_r) with Python's min (tau/0 -> 1, NaN -> 1).
+ * seg is a HOST array of nseg+1 column offsets (seg[0] = 0, seg[nseg] = d).
+ * norm (optional, k doubles) receives norm_r.
+ * Replaces simulate.py:352-356 (bucketing) and :374-378 (history). */
+int sra_clip_scale_f32(const float* M, int64_t k, int64_t d, int64_t ldm, const double* prev, const int64_t* seg,
+                       int32_t nseg, double tau, double* scale, double* norm, void* ws, size_t ws_bytes,
+                       void* stream);
+int sra_clip_scale_f64(const double* M, int64_t k, int64_t d, int64_t ldm, const double* prev, const int64_t* seg,
+                       int32_t nseg, double tau, double* scale, double* norm, void* ws, size_t ws_bytes,
+                       void* stream);
+
+/* out[j] = (sum_r (M[r,j] - prev[j]) * scale[r]) / k in fp64, summed sequentially
+ * over r (np.average(axis=0) of the clipped rows, simulate.py:358-364 / 380-386).
+ * clipped (optional, k x d fp64, row stride ldc) receives the clipped rows -- the
+ * arrays icml2021_history stores back into local_grads (simulate.py:380). */
+int sra_clipped_mean_f32(const float* M, int64_t k, int64_t d, int64_t ldm, const double* prev, const double* scale,
+                         double* clipped, int64_t ldc, double* out, void* stream);
+int sra_clipped_mean_f64(const double* M, int64_t k, int64_t d, int64_t ldm, const double* prev, const double* scale,
+                         double* clipped, int64_t ldc, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

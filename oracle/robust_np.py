@@ -469,6 +469,57 @@ def history_round(layers_by_client, prev, tau):
     return [np.array([g[l] for g in layers_by_client]).mean(axis=0) for l in range(nlayer)]
 
 
+def dispatch_round(agg, local_grads, choices, args, prev):
+    """One round of the reference's per-layer dispatch, simulate.py:231-398
+    (the 14 ``--agg`` branches of simulate.py:76).  ``local_grads[c][l]`` is
+    client c's layer l; ``choices`` the round's client array (shuffled in place
+    on the first iclr2022_bucketing round, simulate.py:338-342).  Returns
+    ``(average_grad, prev_average_grad)``; icml2021_history mutates
+    ``local_grads`` like the reference (simulate.py:380)."""
+    nlayer = len(local_grads[int(choices[0])])
+
+    def layer(l):
+        return [local_grads[c][l] for c in choices]
+
+    eps = args.malnum * 1. / args.nworker
+    if agg == "average":                                            # :235-244
+        return [np.average(np.array(layer(l)), axis=0) for l in range(nlayer)], prev
+    if agg == "krum":                                               # :245-253
+        return [krum(layer(l), f=args.malnum)[0] for l in range(nlayer)], prev
+    if agg == "filterl2":                                           # :254-262
+        return [filterL2(layer(l), eps=eps, sigma=args.sigma) for l in range(nlayer)], prev
+    if agg == "mom_filterl2":                                       # :263-271
+        return [mom_filterL2(layer(l), eps=eps, sigma=args.sigma, delta=np.exp(-50 + args.malnum))
+                for l in range(nlayer)], prev
+    if agg == "median":                                             # :272-280
+        return [median(layer(l)) for l in range(nlayer)], prev
+    if agg == "trimmedmean":                                        # :281-289
+        return [trimmed_mean(layer(l)) for l in range(nlayer)], prev
+    if agg in ("bulyankrum", "bulyanmedian", "bulyantrimmedmean"):  # :290-316
+        sub = agg[len("bulyan"):]
+        return [bulyan(layer(l), args.malnum, aggsubfunc=sub) for l in range(nlayer)], prev
+    if agg == "ex_noregret":                                        # :317-325
+        return [ex_noregret(layer(l), eps=eps, sigma=args.sigma) for l in range(nlayer)], prev
+    if agg == "mom_ex_noregret":                                    # :326-334
+        return [mom_ex_noregret(layer(l), eps=eps, sigma=args.sigma, delta=np.exp(-50 + args.malnum))
+                for l in range(nlayer)], prev
+    if agg == "iclr2022_bucketing":                                 # :335-366
+        if prev is None:
+            prev = [np.zeros(np.shape(local_grads[int(choices[0])][l])) for l in range(nlayer)]
+            for _ in range(nlayer):
+                np.random.shuffle(choices)
+        out = bucketing_round([local_grads[c] for c in choices], prev, args.buckets, args.perround, args.tau)
+        return out, [a.copy() for a in out]
+    if agg == "icml2021_history":                                   # :367-388
+        if prev is None:
+            prev = [np.zeros(np.shape(local_grads[int(choices[0])][l])) for l in range(nlayer)]
+        out = history_round([local_grads[c] for c in choices], prev, args.tau)
+        return out, [a.copy() for a in out]
+    if agg == "clustering":                                         # :389-397
+        return [mom_krum(layer(l), f=args.malnum) for l in range(nlayer)], prev
+    raise ValueError("unknown aggregator %r" % agg)
+
+
 def as_float32_rows(samples):
     """Convenience for tests/bench: (N, D) float32 C-contiguous copy."""
     rows, _ = _as_rows(samples)
@@ -481,5 +532,5 @@ __all__ = [
     "filterL2", "mom_filterL2", "ex_noregret_", "ex_noregret", "mom_ex_noregret",
     "pairwise_l2", "krum_scores_from_dist", "bucket_count", "bucket_means",
     "chunk_sizes", "bulyan_coordinates", "bulyan_select", "kl_capped_projection",
-    "bucketing_round", "history_round",
+    "bucketing_round", "history_round", "dispatch_round",
 ]

@@ -232,10 +232,12 @@ def ex_noregret(X, eps=1. / 12, sigma=1, expansion=20, itv=ITV, check=True):
 
 
 def mom_bucket_count(n, eps, delta):
-    """robust_estimator.py:136-137 / 211-212, evaluated in float64 like numpy."""
-    import math
-    num = int(math.floor(eps * n) + math.log(1. / delta))
-    size = int(math.ceil(n * 1. / num))
+    """robust_estimator.py:136-137 / 211-212, evaluated with numpy's float64
+    floor/log/ceil exactly as the reference (int() truncates a log(1/delta)
+    that lands one ulp below an integer)."""
+    import numpy as np
+    num = int(np.floor(eps * n) + np.log(1. / delta))
+    size = int(np.ceil(n * 1. / num))
     return num, size
 
 
@@ -249,3 +251,93 @@ def mom_ex_noregret(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.71828182
     n = int(X.shape[0])
     num, size = mom_bucket_count(n, eps, delta)
     return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check)
+
+
+# ---------------------------------------------------------------------------
+# cross-layer-norm clipping (k7): iclr2022_bucketing / icml2021_history
+# ---------------------------------------------------------------------------
+_SUFFIX = {torch.float32: "f32", torch.float64: "f64"}
+
+
+def as_rows(X):
+    """Validate an (k, d) CUDA float32/float64 matrix with unit column stride."""
+    if not isinstance(X, torch.Tensor) or not X.is_cuda:
+        raise TypeError("engine ops need a CUDA (HIP) tensor, got %r" % type(X))
+    if X.dtype not in _SUFFIX:
+        raise TypeError("clipping ops take float32 or float64 rows, got %s" % X.dtype)
+    if X.dim() != 2:
+        raise ValueError("expected a (k, d) matrix, got shape %s" % (tuple(X.shape),))
+    if X.shape[1] > 1 and X.stride(1) != 1:
+        X = X.contiguous()
+    k, d = X.shape
+    ld = X.stride(0) if k > 1 else d
+    return X, int(k), int(d), int(max(ld, d))
+
+
+def window_means(X, stride, width, nwin, out=None):
+    """out[w] = mean of rows [w*stride, min(w*stride+width, N)) in X's precision
+    (sequential sum / count, numpy's np.average(axis=0)); (nwin, d)."""
+    X, n, d, ldx = as_rows(X)
+    if out is None:
+        out = torch.empty((nwin, d), dtype=X.dtype, device=X.device)
+    _lib.call("sra_window_mean_" + _SUFFIX[X.dtype], X.data_ptr(), n, d, ldx, int(stride), int(width), int(nwin),
+              out.data_ptr(), out.stride(0), _stream_ptr(X.device))
+    return out
+
+
+def _seg_table(seg, d):
+    import ctypes
+    seg = [int(s) for s in seg] if seg is not None else [0, d]
+    arr = (ctypes.c_int64 * len(seg))(*seg)
+    return arr, len(seg) - 1
+
+
+def clip_scales(M, prev, seg, tau, norms=False):
+    """scale[r] = min(1, tau / ||M[r] - prev||) with the norm across the layer
+    segments ``seg`` (offsets, host ints) as simulate.py:352-356 / 374-378
+    evaluate it.  Returns the (k,) fp64 device tensor (and the norms)."""
+    M, k, d, ldm = as_rows(M)
+    prev = prev.reshape(-1)
+    if prev.dtype != torch.float64 or prev.numel() != d or not prev.is_contiguous():
+        raise ValueError("prev must be a contiguous float64 vector of d elements")
+    arr, nseg = _seg_table(seg, d)
+    nb = _lib.query_bytes("sra_clip_workspace_bytes", k, arr, nseg)
+    ws = _workspace(nb, M.device)
+    scale = torch.empty(k, dtype=torch.float64, device=M.device)
+    nrm = torch.empty(k, dtype=torch.float64, device=M.device) if norms else None
+    _lib.call("sra_clip_scale_" + _SUFFIX[M.dtype], M.data_ptr(), k, d, ldm, prev.data_ptr(), arr, nseg, float(tau),
+              scale.data_ptr(), nrm.data_ptr() if nrm is not None else None, ws.data_ptr(), nb,
+              _stream_ptr(M.device))
+    return (scale, nrm) if norms else scale
+
+
+def clipped_mean(M, prev, scale, clipped=None, out=None):
+    """out = mean_r (M[r] - prev) * scale[r] in fp64 (sequential over r); the
+    clipped rows are written to ``clipped`` ((k, d) fp64) when given."""
+    M, k, d, ldm = as_rows(M)
+    prev = prev.reshape(-1)
+    if out is None:
+        out = torch.empty(d, dtype=torch.float64, device=M.device)
+    ldc = 0
+    if clipped is not None:
+        if clipped.dtype != torch.float64 or tuple(clipped.shape) != (k, d) or clipped.stride(1) != 1:
+            raise ValueError("clipped must be a (k, d) float64 matrix with unit column stride")
+        ldc = clipped.stride(0) if k > 1 else d
+    _lib.call("sra_clipped_mean_" + _SUFFIX[M.dtype], M.data_ptr(), k, d, ldm, prev.data_ptr(), scale.data_ptr(),
+              clipped.data_ptr() if clipped is not None else None, ldc, out.data_ptr(), _stream_ptr(M.device))
+    return out
+
+
+def bucketing(X, prev, seg, buckets, tau):
+    """iclr2022_bucketing (simulate.py:343-364) over the rows of X, already in
+    (shuffled) choices order: overlapping windows X[b : b + N//buckets], clip
+    each window mean against prev by its cross-layer norm, mean over windows."""
+    n = int(X.shape[0])
+    W = window_means(X, 1, n // int(buckets), int(buckets))
+    return clipped_mean(W, prev, clip_scales(W, prev, seg, tau))
+
+
+def history(X, prev, seg, tau, clipped=None):
+    """icml2021_history (simulate.py:374-386): clip every row against prev by
+    its cross-layer norm (written to ``clipped`` when given), mean over rows."""
+    return clipped_mean(X, prev, clip_scales(X, prev, seg, tau), clipped=clipped)
