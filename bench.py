@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 import srfl_loader  # noqa: E402
 
 srfl = srfl_loader.load()
-from srfl_amd import engine  # noqa: E402
+from srfl_amd import engine, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--chunks", type=int, default=16,
+                    help="N>1: all-gather rounds per step (block-cyclic shard, gather of block k "
+                         "overlapped with the aggregation of block k+1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -227,8 +230,17 @@ def main():
     out = torch.empty(d, dtype=odt, device=device)
     full = torch.empty(d * world, dtype=odt, device=device) if world > 1 else None
     fn = AGG[a.agg]
+    # N>1, coordinate-wise: block-cyclic shard (this rank's X = its blocks side
+    # by side) with the in-place all-gather of block k on a second stream,
+    # overlapped with the k-select of block k+1 (srfl_amd/shard.py)
+    pipelined = world > 1 and a.agg in ("trimmedmean", "median", "average") and d % a.chunks == 0
+    comm = torch.cuda.Stream(device=device) if pipelined else None
+    into = shard.engine_ops()[a.agg + "_into"] if pipelined else None
 
     def step(ev=None):
+        if pipelined:
+            shard.pipelined_coordinatewise(into, X, d * world, d // a.chunks, out=full, comm_stream=comm)
+            return
         if ev is not None:
             ev[0].record()
         fn(X, out)
@@ -255,6 +267,13 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if pipelined:
+        # roofline: this rank's local aggregation alone (no collective), same launch
+        for k in range(a.steps):
+            evs[k][0].record()
+            fn(X, out)
+            evs[k][1].record()
+        torch.cuda.synchronize()
     kern_ms = sum(s.elapsed_time(e) for s, e in evs) / a.steps
     ms_per_step = elapsed * 1e3 / a.steps
     total_bytes = n * d * world * 4
@@ -288,7 +307,8 @@ def main():
         "config": {"workload": "%s N=%d clients x d=%.0e fp32 per GPU%s" % (
                        a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
-                   "parallelism": "d-shard x%d" % world},
+                   "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, a.chunks)
+                                   if pipelined else "d-shard x%d" % world)},
         "roofline": {"bound": bound, "kernel": KERNEL_NAME[a.agg], "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic, "kernel_ms": round(kern_ms, 4),

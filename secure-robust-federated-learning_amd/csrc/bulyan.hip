@@ -190,6 +190,85 @@ __global__ void __launch_bounds__(256) row_dist_partial_kernel(const float* __re
   if (threadIdx.x == 0) partial[static_cast<int64_t>(rp) * kDistChunks + c] = red[0];
 }
 
+// RB rows of the list per block over one coordinate chunk: the aggregate's
+// float4 is loaded once for RB rows (it used to be re-read by every row's
+// block), the rows are streamed with non-temporal loads.  Per row the
+// accumulation order is exactly row_dist_partial_kernel<true>'s (elements j,
+// j+1024, ... into four component sums, then the same fixed tree), so the
+// partial sums are bit-identical.
+template <int RB>
+__global__ void __launch_bounds__(256) row_dist_multi_kernel(const float* __restrict__ X, int64_t ldx,
+                                                            const int* __restrict__ rows, int nr, int64_t d,
+                                                            const float* __restrict__ agg, int64_t chunk,
+                                                            float* __restrict__ partial) {
+  const int c = blockIdx.x;
+  const int rp0 = blockIdx.y * RB;
+  const f32x4* x[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int rr = rp0 + r < nr ? rp0 + r : nr - 1;
+    x[r] = reinterpret_cast<const f32x4*>(X + static_cast<int64_t>(rows[rr]) * ldx);
+  }
+  const f32x4* a4 = reinterpret_cast<const f32x4*>(agg);
+  const int64_t j0 = static_cast<int64_t>(c) * chunk;
+  const int64_t j1 = j0 + chunk < d ? j0 + chunk : d;
+  float s[RB][4];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) s[r][0] = s[r][1] = s[r][2] = s[r][3] = 0.f;
+  int64_t j = j0 + 4 * threadIdx.x;
+  for (; j + 1024 + 3 < j1; j += 2 * 1024) {
+    f32x4 aa[2], xa[RB][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      aa[u] = a4[(j + 1024 * u) / 4];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) xa[r][u] = __builtin_nontemporal_load(x[r] + (j + 1024 * u) / 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const f32x4 df = aa[u] - xa[r][u];
+        s[r][0] = __builtin_fmaf(df[0], df[0], s[r][0]);
+        s[r][1] = __builtin_fmaf(df[1], df[1], s[r][1]);
+        s[r][2] = __builtin_fmaf(df[2], df[2], s[r][2]);
+        s[r][3] = __builtin_fmaf(df[3], df[3], s[r][3]);
+      }
+    }
+  }
+  for (; j + 3 < j1; j += 1024) {
+    const f32x4 aa = a4[j / 4];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const f32x4 df = aa - __builtin_nontemporal_load(x[r] + j / 4);
+      s[r][0] = __builtin_fmaf(df[0], df[0], s[r][0]);
+      s[r][1] = __builtin_fmaf(df[1], df[1], s[r][1]);
+      s[r][2] = __builtin_fmaf(df[2], df[2], s[r][2]);
+      s[r][3] = __builtin_fmaf(df[3], df[3], s[r][3]);
+    }
+  }
+  for (int64_t q = j; q < j1 && q < j + 4; ++q) {   // ragged tail of the chunk
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const float df = agg[q] - reinterpret_cast<const float*>(x[r])[q];
+      s[r][0] = __builtin_fmaf(df, df, s[r][0]);
+    }
+  }
+  __shared__ float red[RB][256];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) red[r][threadIdx.x] = (s[r][0] + s[r][1]) + (s[r][2] + s[r][3]);
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) red[r][threadIdx.x] += red[r][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < RB && rp0 + static_cast<int>(threadIdx.x) < nr)
+    partial[static_cast<int64_t>(rp0 + threadIdx.x) * kDistChunks + c] = red[threadIdx.x][0];
+}
+
 // argmin (first strict minimum, NaN never chosen) of the listed rows'
 // distances; removes it from the list (order preserved) into rows_next.
 __global__ void __launch_bounds__(256) bulyan_pick_kernel(const float* __restrict__ partial, const int* __restrict__ rows,
@@ -441,8 +520,8 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
     }
     if (rc) return rc;
     if (dist_vec)
-      hipLaunchKernelGGL(row_dist_partial_kernel<true>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg,
-                         chunk, partial);
+      hipLaunchKernelGGL(row_dist_multi_kernel<4>, dim3(nchunks, cdiv(nr, 4)), dim3(256), 0, s, X, ldx, cur, nr, d,
+                         agg, chunk, partial);
     else
       hipLaunchKernelGGL(row_dist_partial_kernel<false>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg,
                          chunk, partial);

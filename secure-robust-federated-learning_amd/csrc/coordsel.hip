@@ -23,6 +23,7 @@
 // N > 128 (e.g. the N=512 MoM/8-GPU config) uses an LDS bitonic path.
 #include "sra_common.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace sra {
@@ -180,6 +181,206 @@ __global__ void __launch_bounds__(BS) select_reg_kernel(const float* __restrict_
     if (nan_cnt > n - hi) res = qnan();   // a NaN sits in the kept range
   }
   if (t < rem) out[base + t] = res;
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA path (exact N = NX, NX % 4 == 0, NX <= 128): persistent waves, one per
+// SIMD (a 256-thread workgroup per CU).  Each wave owns a private LDS tile of
+// NX rows x 64 coordinates (NX*256 bytes, 32 KiB at N=128) and walks the column
+// tiles t = wave, wave + W, ... :
+//   1. wait for tile t's LDS-DMA (s_waitcnt vmcnt(0): the wave's only VMEM
+//      operations in flight are that DMA and the previous tile's store);
+//   2. read its column into VGPRs (ds_read, lane = coordinate: conflict-free);
+//   3. issue the DMA of tile t+W into the same buffer -- NX/4
+//      global_load_lds_dwordx4, 1 KiB each (4 rows x 256 B, coalesced) -- so the
+//      HBM fetch of the next tile runs under
+//   4. the NaN check, the selection network and the ascending-order sum of
+//      tile t (the same code as select_reg_kernel: bit-identical results).
+// The fetch is decoupled from the register file (no VGPRs hold in-flight
+// data), so the wave never waits on HBM once the pipeline is primed and the
+// column's ~3k VALU ops overlap the next tile's 32 KiB fetch completely.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// One global_load_lds_dwordx4: 64 lanes x 16 B from the wave-uniform row base
+// `rows4` (SGPR pair) + each lane's 32-bit byte offset into LDS at
+// lds_base + I*1024 (M0 is set and restored inside the statement; hipcc does
+// not count asm loads -- the kernel waits with an explicit vmcnt(0)).
+template <int I>
+__device__ __forceinline__ void dma16(uint64_t rows4, unsigned lane_off, uint32_t lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %4\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep) : "v"(lane_off), "s"(rows4), "s"(lds_base), "i"(I * 1024) : "memory");
+}
+
+__device__ __forceinline__ void opaque_sgpr(uint64_t& p) { asm volatile("" : "+s"(p)); }
+
+template <int... I>
+__device__ __forceinline__ void dma_rows(uint64_t p, uint64_t step4, unsigned lane_off, uint32_t lds_base,
+                                         std::integer_sequence<int, I...>) {
+  // a running SGPR row pointer (opaque to the optimiser, so it is not
+  // rematerialised as NX/4 hoisted 64-bit offsets)
+  ((dma16<I>(p, lane_off, lds_base), p += step4, opaque_sgpr(p)), ...);
+}
+
+// tile t = columns [64t, 64t+64) of all NX rows -> the wave's LDS tile
+template <int NX>
+__device__ __forceinline__ void dma_tile(const float* X, int64_t t, uint64_t step4, unsigned lane_off,
+                                         uint32_t lds_base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(X + t * kWave);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  dma_rows((static_cast<uint64_t>(hi) << 32) | lo, step4, lane_off, lds_base,
+           std::make_integer_sequence<int, NX / 4>{});
+}
+
+template <int MODE, int NX, int BX>
+__global__ void __launch_bounds__(256, 1) select_dma_kernel(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
+                                                           float* __restrict__ out) {
+  static_assert(NX % 4 == 0 && NX <= 128, "exact-N DMA path");
+  extern __shared__ __attribute__((aligned(16))) float lds_tiles[];
+  constexpr int P = ((NX + 15) / 16) * 16;
+  constexpr int P2 = next_pow2(P);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63u;
+  float* buf = lds_tiles + wave * (NX * kWave);
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)buf);
+  const int64_t ldb = ldx * 4;
+  const uint64_t step4 = static_cast<uint64_t>(ldb) * 4;
+  const unsigned lane_off = static_cast<unsigned>((lane >> 4) * ldb) + (lane & 15u) * 16u;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * 4;
+  int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+  if (t >= ntiles) return;
+  dma_tile<NX>(X, t, step4, lane_off, lds_base);
+
+  constexpr int kMedLo = (NX - 1) / 2;
+  constexpr int kMedHi = NX / 2;
+  constexpr int kOutLo = MODE == kMedian ? kMedLo : BX;
+  constexpr int kOutHi = MODE == kMedian ? kMedHi + 1 : NX - BX;
+  for (; t < ntiles; t += step) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float v[P2];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) v[i] = buf[i * kWave + lane];
+    // every lane's reads have returned before the DMA may overwrite the tile
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + step < ntiles) dma_tile<NX>(X, t + step, step4, lane_off, lds_base);
+
+    float m = v[0];
+#pragma unroll
+    for (int i = 1; i < NX; ++i) m = __builtin_elementwise_maximum(m, v[i]);
+    int nan_cnt = 0;
+    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        const bool isn = __builtin_isnan(v[i]);
+        nan_cnt += isn ? 1 : 0;
+        v[i] = isn ? __builtin_inff() : v[i];
+      }
+    }
+    network_fast<P2, NX, kOutLo, kOutHi>(v);
+    float res;
+    if constexpr (MODE == kMedian) {
+      res = (NX & 1) ? v[kMedLo] : (v[kMedLo] + v[kMedHi]) * 0.5f;
+      if (nan_cnt > 0) res = qnan();
+    } else {
+      float acc = 0.f;
+#pragma unroll
+      for (int p = BX; p < NX - BX; ++p) acc += v[p];
+      res = acc / static_cast<float>(NX - 2 * BX);
+      if (nan_cnt > BX) res = qnan();
+    }
+    out[t * kWave + lane] = res;
+  }
+}
+
+// Two-waves-per-SIMD variant (one 512-thread workgroup per CU): rows [0, H) of
+// the next tile arrive by LDS-DMA into a 16 KiB per-wave buffer, rows [H, NX)
+// by plain loads into VGPRs (pf); both are issued right after the current
+// tile was read, so the fetch overlaps the network and two waves share each
+// SIMD's VALU issue (one wave alone issues a VALU op every 4 cycles, the
+// SIMD-32 can take one every 2).
+template <int MODE, int NX, int BX>
+__global__ void __launch_bounds__(512) select_dma2_kernel(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
+                                                         float* __restrict__ out) {
+  static_assert(NX <= 128, "exact-N DMA path");
+  constexpr int H = (NX / 2) & ~3;   // rows fetched by LDS-DMA (4 per instruction)
+  constexpr int R = NX - H;          // rows prefetched into VGPRs
+  extern __shared__ __attribute__((aligned(16))) float lds_tiles2[];
+  constexpr int P = ((NX + 15) / 16) * 16;
+  constexpr int P2 = next_pow2(P);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned lane = threadIdx.x & 63u;
+  float* buf = lds_tiles2 + wave * (H * kWave);
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)buf);
+  const int64_t ldb = ldx * 4;
+  const uint64_t step4 = static_cast<uint64_t>(ldb) * 4;
+  const unsigned lane_off = static_cast<unsigned>((lane >> 4) * ldb) + (lane & 15u) * 16u;
+  const unsigned col_off = lane * 4u;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * 8;
+  int64_t t = static_cast<int64_t>(blockIdx.x) * 8 + wave;
+  if (t >= ntiles) return;
+  float pf[R];
+  auto prefetch = [&](int64_t tt) {
+    dma_tile<H>(X, tt, step4, lane_off, lds_base);
+    // running SGPR row pointer (opaque: no R hoisted 64-bit row offsets)
+    const uint64_t a = reinterpret_cast<uint64_t>(X + tt * kWave + H * ldx);
+    const uint32_t alo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));        // (int -> uint32: no
+    const uint32_t ahi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));  //  sign extension)
+    uint64_t rp = (static_cast<uint64_t>(ahi) << 32) | alo;
+    typedef const __attribute__((address_space(1))) float gfloat;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      pf[i] = __builtin_nontemporal_load(reinterpret_cast<gfloat*>(rp + col_off));
+      rp += static_cast<uint64_t>(ldb);
+      opaque_sgpr(rp);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  prefetch(t);
+
+  constexpr int kMedLo = (NX - 1) / 2;
+  constexpr int kMedHi = NX / 2;
+  constexpr int kOutLo = MODE == kMedian ? kMedLo : BX;
+  constexpr int kOutHi = MODE == kMedian ? kMedHi + 1 : NX - BX;
+  for (; t < ntiles; t += step) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float v[P2];
+#pragma unroll
+    for (int i = 0; i < H; ++i) v[i] = buf[i * kWave + lane];
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[H + i] = pf[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + step < ntiles) prefetch(t + step);
+
+    float m = v[0];
+#pragma unroll
+    for (int i = 1; i < NX; ++i) m = __builtin_elementwise_maximum(m, v[i]);
+    int nan_cnt = 0;
+    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        const bool isn = __builtin_isnan(v[i]);
+        nan_cnt += isn ? 1 : 0;
+        v[i] = isn ? __builtin_inff() : v[i];
+      }
+    }
+    network_fast<P2, NX, kOutLo, kOutHi>(v);
+    float res;
+    if constexpr (MODE == kMedian) {
+      res = (NX & 1) ? v[kMedLo] : (v[kMedLo] + v[kMedHi]) * 0.5f;
+      if (nan_cnt > 0) res = qnan();
+    } else {
+      float acc = 0.f;
+#pragma unroll
+      for (int p = BX; p < NX - BX; ++p) acc += v[p];
+      res = acc / static_cast<float>(NX - 2 * BX);
+      if (nan_cnt > BX) res = qnan();
+    }
+    out[t * kWave + lane] = res;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -355,6 +556,14 @@ __global__ void __launch_bounds__(256) select_lds_kernel(const float* __restrict
   }
 }
 
+static int64_t num_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return 256;
+  return cus;
+}
+
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return (e != nullptr && e[0] != 0) ? atoi(e) : dflt;
@@ -391,6 +600,43 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
     if (n <= 128) SRA_SEL2(64, 0, -1);
     SRA_SEL2(128, 0, -1);
 #undef SRA_SEL2
+  }
+  const bool dma_ok = force != 1 && force != 2 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+                      d >= kWave && ldx * 4 * 4 < (int64_t(1) << 32);   // 32-bit DMA lane offsets (rows 0..3)
+  // LDS-DMA persistent variants: off by default -- measured slower than the
+  // register path at N = 100 / 128, d = 1e8; SRA_DMA_WAVES=1|2
+  // selects them for A/B runs.
+  static const int dma_waves = env_int("SRA_DMA_WAVES", 0);
+  if (dma_ok && dma_waves > 0 && (trim128 || trim100 || (MODE == kMedian && (n == 128 || n == 100)))) {
+    const int64_t ntiles = d / kWave;
+#define SRA_DMA(NXX, BXX)                                                                                        \
+  do {                                                                                                           \
+    const bool one = dma_waves == 1;                                                                             \
+    auto kern = one ? select_dma_kernel<MODE, NXX, BXX> : select_dma2_kernel<MODE, NXX, BXX>;                    \
+    const int wpb = one ? 4 : 8;                                                                                 \
+    const int lds1 = 4 * NXX * kWave * static_cast<int>(sizeof(float));                                          \
+    const int lds2 = 8 * ((NXX / 2) & ~3) * kWave * static_cast<int>(sizeof(float));                            \
+    static const hipError_t attr1 = hipFuncSetAttribute(                                                         \
+        reinterpret_cast<const void*>(select_dma_kernel<MODE, NXX, BXX>),                                       \
+        hipFuncAttributeMaxDynamicSharedMemorySize, lds1);                                                       \
+    static const hipError_t attr2 = hipFuncSetAttribute(                                                         \
+        reinterpret_cast<const void*>(select_dma2_kernel<MODE, NXX, BXX>),                                      \
+        hipFuncAttributeMaxDynamicSharedMemorySize, lds2);                                                       \
+    if ((one ? attr1 : attr2) != hipSuccess) break;                                                              \
+    const int64_t grid = std::min<int64_t>(num_cus(), cdiv(ntiles, wpb));                                        \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * wpb), one ? lds1 : lds2, s, X, ntiles, ldx, out);             \
+    int rc = launch_status("select_dma_kernel");                                                                 \
+    if (rc || d % kWave == 0) return rc;                                                                         \
+    return launch_select<MODE>(X + ntiles * kWave, n, d - ntiles * kWave, ldx, lo, hi, out + ntiles * kWave, s); \
+  } while (0)
+    if constexpr (MODE == kTrimmed) {
+      if (trim128) SRA_DMA(128, 12);
+      if (trim100) SRA_DMA(100, 10);
+    } else {
+      if (n == 128) SRA_DMA(128, -1);
+      if (n == 100) SRA_DMA(100, -1);
+    }
+#undef SRA_DMA
   }
   if (n <= 128) {
     const int bs = bs_env == 768 ? 768 : 256;

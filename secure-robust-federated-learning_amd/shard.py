@@ -88,6 +88,77 @@ def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
     return row, idx
 
 
+# ---------------------------------------------------------------------------
+# block-cyclic sharding with a pipelined, overlapped all-gather
+# ---------------------------------------------------------------------------
+def cyclic_blocks(d, world, rank, block):
+    """Global column ranges owned by ``rank`` under block-cyclic sharding:
+    global block g = [g*block, min((g+1)*block, d)) belongs to rank g % world.
+    Returned in the rank's local order (local block k = global block
+    k*world + rank)."""
+    if world < 1 or not 0 <= rank < world or block < 1:
+        raise ValueError("bad world/rank/block %d/%d/%d" % (world, rank, block))
+    nb = -(-int(d) // int(block))
+    return [(g * block, min((g + 1) * block, d)) for g in range(rank, nb, world)]
+
+
+def cyclic_rounds(d, world, block):
+    """Number of all-gather rounds (one global block per rank per round)."""
+    nb = -(-int(d) // int(block))
+    return -(-nb // world)
+
+
+def pipelined_coordinatewise(local_fn, X_local, d, block, group=None, out=None, comm_stream=None):
+    """Coordinate-wise (or per-chunk) aggregation of a block-cyclic shard with
+    the all-gather of block k overlapped with the aggregation of block k+1.
+
+    ``X_local``: (N, sum of widths) -- this rank's blocks (``cyclic_blocks``)
+    side by side.  ``local_fn(X_cols, out_view)`` aggregates one block into
+    ``out_view`` (1-D, that block's width).  Round k's results land in
+    ``full[k*world*block + rank*block ...]`` -- exactly their global positions,
+    so each round is one IN-PLACE all-gather of ``world*block`` elements and no
+    reordering copy follows.  On a GPU the collectives run on ``comm_stream``
+    (RCCL over xGMI), ordered after the block's aggregation by an event; the
+    aggregation of the next block proceeds concurrently on the current stream.
+    Returns the (d,) aggregate on every rank."""
+    world, rank = _world(group) if dist.is_initialized() else (1, 0)
+    rounds = cyclic_rounds(d, world, block)
+    span = world * block
+    full = out
+    if full is None or full.numel() < rounds * span:
+        full = torch.empty(rounds * span, dtype=_out_dtype(local_fn, X_local), device=X_local.device)
+    mine = cyclic_blocks(d, world, rank, block)
+    cuda = X_local.is_cuda and world > 1
+    compute = torch.cuda.current_stream(X_local.device) if cuda else None
+    if cuda and comm_stream is None:
+        comm_stream = torch.cuda.Stream(device=X_local.device)
+    off = 0
+    for k in range(rounds):
+        seg = full[k * span + rank * block: k * span + (rank + 1) * block]
+        if k < len(mine):
+            lo, hi = mine[k]
+            local_fn(X_local[:, off:off + hi - lo], seg[:hi - lo])
+            off += hi - lo
+        if world == 1:
+            continue
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(compute)
+            with torch.cuda.stream(comm_stream):
+                comm_stream.wait_event(ev)
+                dist.all_gather_into_tensor(full[k * span:(k + 1) * span], seg, group=group)
+        else:
+            dist.all_gather_into_tensor(full[k * span:(k + 1) * span], seg, group=group)
+    if cuda:
+        compute.wait_stream(comm_stream)
+        full.record_stream(comm_stream)
+    return full[:d]
+
+
+def _out_dtype(local_fn, X):
+    return getattr(local_fn, "out_dtype", X.dtype)
+
+
 def engine_ops():
     """The HIP-backed per-shard operations (GPU ranks)."""
     from . import engine
@@ -105,6 +176,10 @@ def engine_ops():
         "trimmedmean": lambda X: engine.trimmed_mean(X, 0.1),
         "gram": gram_fn,
         "krum_select": select_fn,
+        # (X_cols, out_view) forms for pipelined_coordinatewise
+        "average_into": lambda X, o: engine.average(X, out=o),
+        "median_into": lambda X, o: engine.median(X, out=o),
+        "trimmedmean_into": lambda X, o: engine.trimmed_mean(X, 0.1, out=o),
     }
 
 

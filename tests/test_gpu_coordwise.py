@@ -90,3 +90,25 @@ def test_full_size_properties():
     np.testing.assert_array_equal(md[:100_000].cpu().numpy(), orc.median(list(sl)))
     out = gre.trimmed_mean(X)            # device in -> device out
     assert out.is_cuda and torch.equal(out, tm)
+
+
+@pytest.mark.parametrize("n", [100, 128])
+@pytest.mark.parametrize("d,ldx", [(64, 64), (65, 68), (1031, 1040), (300_000, 300_000), (299_999, 300_004)])
+def test_lds_dma_path_bitexact(n, d, ldx):
+    """The persistent LDS-DMA k-select (exact N = 100 / 128; several tiles per
+    wave, a partial last tile served by the register path, padded rows) with
+    NaN / inf columns, against the oracle."""
+    import warnings
+    rng = np.random.default_rng(n + d)
+    full = make_rows(n, ldx, seed=d + n)
+    full[rng.integers(0, n, 40), rng.integers(0, d, 40)] = np.nan
+    full[rng.integers(0, n, 40), rng.integers(0, d, 40)] = np.inf
+    full[rng.integers(0, n, 40), rng.integers(0, d, 40)] = -np.inf
+    col = int(rng.integers(0, d))
+    full[: n // 5, col] = np.nan              # more NaNs than the trim count -> NaN
+    X = torch.from_numpy(full).cuda()[:, :d]
+    x = full[:, :d]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        np.testing.assert_array_equal(engine.trimmed_mean(X).cpu().numpy(), orc.trimmed_mean(list(x)))
+        np.testing.assert_array_equal(engine.median(X).cpu().numpy(), orc.median(list(x)))

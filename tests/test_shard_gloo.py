@@ -84,24 +84,66 @@ def _worker(rank, world, port, results):
         row, idx = shard.krum(lambda X: torch.from_numpy(_centred_gram(X.numpy())), select, Xk, 777, 6)
         out["krum_row"] = row.numpy()
         out["krum_idx"] = idx
+        # block-cyclic shard + pipelined in-place all-gather, ragged last round
+        for block in (64, 96, 1001):
+            cols = shard.cyclic_blocks(d, world, rank, block)
+            Xc = torch.from_numpy(np.ascontiguousarray(np.concatenate([x[:, lo:hi] for lo, hi in cols], axis=1)
+                                                       if cols else x[:, :0]))
+
+            def tm_into(X, o):
+                o.copy_(torch.from_numpy(np.asarray(orc.trimmed_mean(list(X.numpy())))))
+            out["cyclic_%d" % block] = shard.pipelined_coordinatewise(tm_into, Xc, d, block).numpy().copy()
         results[rank] = out
     finally:
         dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def two_rank_results():
+def _run(world):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     results = mgr.dict()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, results)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, results)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=180)
         assert p.exitcode == 0, "gloo worker failed"
     return dict(results)
+
+
+@pytest.fixture(scope="module")
+def two_rank_results():
+    return _run(2)
+
+
+@pytest.fixture(scope="module")
+def three_rank_results():
+    return _run(3)
+
+
+def test_cyclic_blocks_partition():
+    _setup_paths()
+    from srfl_amd import shard
+    for d in (1, 7, 1000, 1001, 12345):
+        for world in (1, 2, 3, 8):
+            for block in (1, 64, 1000):
+                cols = sorted(c for r in range(world) for c in shard.cyclic_blocks(d, world, r, block))
+                assert cols[0][0] == 0 and cols[-1][1] == d
+                assert all(a[1] == b[0] for a, b in zip(cols, cols[1:]))
+                assert shard.cyclic_rounds(d, world, block) * world * block >= d
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_cyclic_equals_unsharded(world, two_rank_results, three_rank_results):
+    _setup_paths()
+    from oracle import robust_np as orc
+    from synth import make_rows
+    res = two_rank_results if world == 2 else three_rank_results
+    want = orc.trimmed_mean(list(make_rows(37, 1001, seed=11, byz=5)))
+    for r in range(world):
+        for block in (64, 96, 1001):
+            np.testing.assert_array_equal(res[r]["cyclic_%d" % block], want)
 
 
 def test_shard_bounds_cover_and_align():

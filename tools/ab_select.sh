@@ -1,15 +1,22 @@
 #!/bin/bash
-# A/B of the k-select variants on the default bench workload (one process each, same box)
+# A/B of the k-select launch variants (trimmed mean N=128 / 100, median N=128,
+# d=1e8): register path (block 256 / 768), two-lane path (block 256 / 1024).
 set -u
-mkdir -p gpurun_out
-AGGS=${AGGS:-trimmedmean median}
-VARIANTS=${VARIANTS:-"1:256 1:768 2:256 2:1024"}
-for agg in $AGGS; do
-  for v in $VARIANTS; do
-    sel=${v%%:*}; bs=${v##*:}
-    f=gpurun_out/ab_${agg}_s${sel}_b${bs}
-    SRA_SELECT=$sel SRA_BS=$bs timeout -k 10 300 python bench.py --agg $agg --steps 10 --warmup 2 --no-cpu --no-host ${BENCH_ARGS:-} \
-      > $f.json 2> $f.err || exit $?
-    python -c "import json;l=json.load(open('$f.json'));print('$agg sel=$sel bs=$bs', l['value'], l['roofline']['kernel_ms'], l['roofline']['frac'])"
-  done
+OUT=${OUT:-gpurun_out/ab_select}
+mkdir -p "$OUT"
+run() { # name env...
+  local name=$1; shift
+  echo "== $name" | tee -a "$OUT/summary.txt"
+  timeout -k 10 240 env "$@" > "$OUT/$name.log" 2>&1 || { echo "FAILED $name rc=$?" | tee -a "$OUT/summary.txt"; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('$OUT/$name.log').read().strip().splitlines()[-1]); r=d['roofline']; print('  value %.1f GB/s  kernel %.3f ms  frac %.4f' % (d['value'], r['kernel_ms'], r['frac']))" | tee -a "$OUT/summary.txt"
+}
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu --no-host"
+for cfg in "trimmedmean 128" "trimmedmean 100" "median 128"; do
+  set -- $cfg
+  agg=$1; n=$2
+  run ${agg}_n${n}_reg256 SRA_SELECT=1 SRA_BS=256 $B --agg $agg --clients $n
+  run ${agg}_n${n}_reg768 SRA_SELECT=1 SRA_BS=768 $B --agg $agg --clients $n
+  run ${agg}_n${n}_two256 SRA_SELECT=2 SRA_BS=256 $B --agg $agg --clients $n
+  run ${agg}_n${n}_two1024 SRA_SELECT=2 SRA_BS=1024 $B --agg $agg --clients $n
 done
+echo "== done" | tee -a "$OUT/summary.txt"
