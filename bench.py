@@ -113,7 +113,7 @@ OUT_DTYPE = {"bulyankrum": torch.float64, "bulyanmedian": torch.float64, "bulyan
              "filterl2": torch.float64, "ex_noregret": torch.float64, "mom_filterl2": torch.float64,
              "mom_ex_noregret": torch.float64}
 KERNEL_NAME = {
-    "trimmedmean": "select_reg_kernel<128, 1, 128, 12>",
+    "trimmedmean": "select_plain_kernel<1, 128, 12>",
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
     "krum": "whole krum op (gram_partial_kernel dominant; per-kernel split in profiles/)",

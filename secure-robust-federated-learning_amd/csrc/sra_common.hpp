@@ -80,13 +80,17 @@ __device__ __forceinline__ void ce(float& a, float& b) {
 // expanded with immediate register indices.
 // ---------------------------------------------------------------------------
 enum NetOpKind : int { kOpCE = 0, kOpMin = 1, kOpMax = 2, kOpMove = 3 };
-enum NetKind : int { kNetSort = 0, kNetMerge = 1 };
+// kNetFrom4: odd-even merges only, for inputs whose aligned blocks of 4 are
+// already sorted (sort4_blocks below does that with 3-input min/med/max).
+enum NetKind : int { kNetSort = 0, kNetMerge = 1, kNetFrom4 = 2 };
 
 template <int P2, int KIND>
 struct BaseNet {
   template <typename F>
   static constexpr void each(F&& f) {
-    if constexpr (KIND == kNetSort) {
+    if constexpr (KIND == kNetFrom4) {
+      from4(f, 0, P2);
+    } else if constexpr (KIND == kNetSort) {
       // depth-first Batcher odd-even merge sort: sort(lo half), sort(hi half),
       // merge.  Same comparators as the stage-major form, but the first rows'
       // sub-sort only reads the first loads, so a wave starts sorting while
@@ -131,14 +135,45 @@ struct BaseNet {
   // each merge (consecutive comparators independent -> wide asm groups and
   // few dependent asm boundaries)
   static constexpr int kBlock = 32;
+  // 16-input sorting network with 60 comparators (Green; the best known size,
+  // 3 fewer than Batcher's 63), 10 layers.  Checked exhaustively with the 0-1
+  // principle in tests/test_networks.py.
+  static constexpr short kGreen16[60][2] = {
+      {0, 13}, {1, 12}, {2, 15}, {3, 14}, {4, 8}, {5, 6}, {7, 11}, {9, 10},
+      {0, 5}, {1, 7}, {2, 9}, {3, 4}, {6, 13}, {8, 14}, {10, 15}, {11, 12},
+      {0, 1}, {2, 3}, {4, 5}, {6, 8}, {7, 9}, {10, 11}, {12, 13}, {14, 15},
+      {0, 2}, {1, 3}, {4, 10}, {5, 11}, {6, 7}, {8, 9}, {12, 14}, {13, 15},
+      {1, 2}, {3, 12}, {4, 6}, {5, 7}, {8, 10}, {9, 11}, {13, 14},
+      {1, 4}, {2, 6}, {5, 8}, {7, 10}, {9, 13}, {11, 14},
+      {2, 4}, {3, 6}, {9, 12}, {11, 13},
+      {3, 5}, {6, 8}, {7, 9}, {10, 12},
+      {3, 4}, {5, 6}, {7, 8}, {9, 10}, {11, 12},
+      {6, 7}, {8, 9}};
   template <typename F>
   static constexpr void sort_hybrid(F& f, int lo, int n) {
+    if (n == 16) {
+      for (int q = 0; q < 60; ++q) f(lo + kGreen16[q][0], lo + kGreen16[q][1]);
+      return;
+    }
+    if (n == 32) {   // 2 x 60 + 65 = 185 comparators (Batcher: 191)
+      sort_hybrid(f, lo, 16);
+      sort_hybrid(f, lo + 16, 16);
+      merge_stages(f, lo, 32);
+      return;
+    }
     if (n <= kBlock) {
       sort_stages(f, lo, n);
       return;
     }
     sort_hybrid(f, lo, n / 2);
     sort_hybrid(f, lo + n / 2, n / 2);
+    merge_stages(f, lo, n);
+  }
+  template <typename F>
+  static constexpr void from4(F& f, int lo, int n) {
+    if (n <= 4) return;
+    from4(f, lo, n / 2);
+    from4(f, lo + n / 2, n / 2);
     merge_stages(f, lo, n);
   }
   template <typename F>
@@ -370,6 +405,55 @@ template <int P2, int PR, int OLO, int OHI, int KIND>
 __device__ __forceinline__ void network_plain(float (&v)[P2]) {
   using Plan = NetPlan<P2, PR, OLO, OHI, KIND>;
   if constexpr (P2 > 1) net_run_plain<Plan>(v, std::make_index_sequence<Plan::value.n>{});
+}
+
+// Sort the aligned blocks of 4 of v[0..PR) (NaN-free) with 7 VALU ops each
+// instead of 5 compare-exchanges (10 ops): a 3-sorter (min3, med3, max3) and
+// an insertion of the 4th value, whose sorted position is
+//   [min(s0,d), med3(s0,s1,d), med3(s1,s2,d), max(s2,d)]  (s0 <= s1 <= s2).
+// Blocks at or beyond PR are compile-time padding and skipped.
+template <int PR, int P2>
+__device__ __forceinline__ void sort4_blocks(float (&v)[P2]) {
+#pragma unroll
+  for (int b = 0; b + 4 <= PR; b += 4) {
+    const float a0 = v[b], a1 = v[b + 1], a2 = v[b + 2], d = v[b + 3];
+    const float s0 = __builtin_fminf(__builtin_fminf(a0, a1), a2);
+    const float s1 = __builtin_amdgcn_fmed3f(a0, a1, a2);
+    const float s2 = __builtin_fmaxf(__builtin_fmaxf(a0, a1), a2);
+    v[b] = __builtin_fminf(s0, d);
+    v[b + 1] = __builtin_amdgcn_fmed3f(s0, s1, d);
+    v[b + 2] = __builtin_amdgcn_fmed3f(s1, s2, d);
+    v[b + 3] = __builtin_fmaxf(s2, d);
+  }
+  static_assert(PR % 4 == 0, "sort4_blocks needs whole blocks");
+}
+
+// As sort4_blocks, but the block maximum (slot 3) is computed with the
+// NaN-PROPAGATING IEEE-754-2019 maximum: a NaN anywhere in a block makes its
+// slot 3 NaN, so a max3 over the slots 3 (PR/8 ops) detects NaNs in the whole
+// column.  The other slots are unspecified when a block holds a NaN (the
+// caller then reloads, maps NaN -> +inf and uses sort4_blocks).
+template <int PR, int P2>
+__device__ __forceinline__ float sort4_blocks_nancheck(float (&v)[P2]) {
+  static_assert(PR % 4 == 0, "sort4_blocks needs whole blocks");
+#pragma unroll
+  for (int b = 0; b + 4 <= PR; b += 4) {
+    const float a0 = v[b], a1 = v[b + 1], a2 = v[b + 2], d = v[b + 3];
+    const float s0 = __builtin_fminf(__builtin_fminf(a0, a1), a2);
+    const float s1 = __builtin_amdgcn_fmed3f(a0, a1, a2);
+    const float s2 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a0, a1), a2);
+    v[b] = __builtin_fminf(s0, d);
+    v[b + 1] = __builtin_amdgcn_fmed3f(s0, s1, d);
+    v[b + 2] = __builtin_amdgcn_fmed3f(s1, s2, d);
+    v[b + 3] = __builtin_elementwise_maximum(s2, d);
+  }
+  float m = v[3];
+#pragma unroll
+  for (int b = 4; b + 4 <= PR; b += 8) {
+    const float hi = b + 4 < PR ? v[b + 7] : v[b + 3];
+    m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m, v[b + 3]), hi);
+  }
+  return m;
 }
 
 // DPP lane exchange with the neighbour lane (quad_perm [1,0,3,2]: 2c <-> 2c+1)
