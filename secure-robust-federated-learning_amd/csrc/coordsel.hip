@@ -611,6 +611,188 @@ __global__ void __launch_bounds__(BS) select2_kernel(const float* __restrict__ X
 }
 
 // ---------------------------------------------------------------------------
+// Multi-lane path for 128 < N <= 512 (the N = 512 MoM / 8-GPU config): L = 2 or
+// 4 lanes share one coordinate, 128 values each, all in registers.
+//   lane (c, h) = lane L*c + h holds rows {L*i + h} of coordinate c (per load
+//   instruction the L rows are consecutive: row base in SGPRs + a 32-bit lane
+//   offset).  Rows >= n are padding (+inf; split -inf/+inf for the median).
+//   1. NaN pre-pass (max3; NaNs counted, mapped to +inf), then each lane
+//      flips its values into its sign domain sigma_h (+,-,-,+): every later
+//      step sorts ASCENDING in the stored domain, a descending run is an
+//      ascending run of negated values;
+//   2. each lane sorts its 128 values (3-input sorted 4-blocks + odd-even
+//      merges, VOP2 min/max);
+//   3. bitonic merges across lanes, one DPP instruction per element:
+//      new = min(own, -partner) is the lower half in one lane and the negated
+//      upper half in the partner, because their domains are opposite
+//      (v_min_f32_dpp with a negated quad_perm source); lanes then flip back
+//      where needed and finish with an in-lane half-cleaner cascade.
+//      L=2: one level (pairs); L=4: pairs, then the 4-lane merge (a stride-256
+//      step between lanes h, h^2 and a stride-128 step between h, h^1).
+//   4. sorted order: L=2: lane0[0..127], lane1[0..127];
+//      L=4: lane0[0..127], lane1[0..127], -lane3[127..0], -lane2[127..0];
+//      the trimmed mean walks it in ascending order with one fp32 accumulator
+//      handed from lane to lane (numpy's sequential sum, bit for bit).
+// Validated in numpy (tools/quad_model.py) before it was written here.
+// ---------------------------------------------------------------------------
+template <int PERM>
+__device__ __forceinline__ float min_neg_partner(float own) {
+  float r;
+  if constexpr (PERM == 1)
+    asm volatile("v_min_f32_dpp %0, -%1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(own));
+  else
+    asm volatile("v_min_f32_dpp %0, -%1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(own));
+  return r;
+}
+
+template <int PERM>
+__device__ __forceinline__ void cross_step(float (&v)[128]) {
+  // DPP reads VGPRs written by VALU: 2 wait states; nothing may move across
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 128; ++i) v[i] = min_neg_partner<PERM>(v[i]);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void flip(float (&v)[128], uint32_t mask) {
+#pragma unroll
+  for (int i = 0; i < 128; ++i) v[i] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v[i]) ^ mask);
+}
+
+// value of `x` in lane h = H of this lane's group of L (quad_perm [H,H,H,H] for
+// L = 4, [H,H,2+H,2+H] for the two pairs of a quad when L = 2)
+template <int L, int H>
+__device__ __forceinline__ float from_lane(float x) {
+  constexpr int ctrl = L == 4 ? (H | (H << 2) | (H << 4) | (H << 6)) : (H | (H << 2) | ((2 + H) << 4) | ((2 + H) << 6));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), ctrl, 0xF, 0xF, false));
+}
+
+template <int L, int MODE, int NX = 0, int BX = -1>
+__global__ void __launch_bounds__(256) select_quad_kernel(const float* __restrict__ X, int n_rt, int64_t d,
+                                                         int64_t ldx, int lo_rt, int hi_rt, float* __restrict__ out) {
+  static_assert(L == 2 || L == 4, "2 or 4 lanes per coordinate");
+  constexpr bool kExactN = NX > 0;
+  constexpr bool kExactB = kExactN && BX >= 0;
+  const int n = kExactN ? NX : n_rt;
+  const int lo = kExactB ? BX : lo_rt;
+  const int hi = kExactB ? NX - BX : hi_rt;
+  constexpr int P = 128 * L;
+  constexpr int CPW = kWave / L;                 // coordinates per wave
+  constexpr int CPB = 4 * CPW;                   // per 256-thread block
+  const unsigned lane = threadIdx.x & 63u;
+  const int h = static_cast<int>(lane % L);
+  const int c = static_cast<int>(threadIdx.x / L);   // coordinate within the block
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * CPB;
+  const int64_t rem = d - base;
+  const int cc = c < rem ? c : static_cast<int>(rem - 1);
+  const uint64_t ldb = static_cast<uint64_t>(ldx) * 4;
+  const unsigned off = static_cast<unsigned>(h * ldb) + static_cast<unsigned>(cc) * 4u;
+  const uint64_t a = reinterpret_cast<uint64_t>(X + base);
+  const uint32_t alo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t ahi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  uint64_t rp = (static_cast<uint64_t>(ahi) << 32) | alo;
+  const uint64_t rstep = ldb * L;
+  typedef const __attribute__((address_space(1))) float gfloat;
+  const int k_bottom = (MODE == kMedian && !kExactN) ? (P - n) / 2 : 0;
+  float v[128];
+#pragma unroll
+  for (int i = 0; i < 128; ++i) {
+    if (kExactN ? (L * i + L - 1 < NX) : (L * i + L - 1 < n)) {     // wave-uniform: all L rows real
+      v[i] = __builtin_nontemporal_load(reinterpret_cast<gfloat*>(rp + off));
+    } else {                                                          // tail: clamp the row, then pad
+      const int row = L * i + h;
+      const int rr = row < n ? row : n - 1;
+      const uint64_t ad = a + static_cast<uint64_t>(rr) * ldb + static_cast<unsigned>(cc) * 4u;
+      const float x = __builtin_nontemporal_load(reinterpret_cast<gfloat*>(ad));
+      const float pad = (row - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
+      v[i] = row < n ? x : pad;
+    }
+    rp += rstep;
+    opaque_sgpr(rp);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // NaN pre-pass
+  float m = v[0];
+#pragma unroll
+  for (int i = 1; i < 128; ++i) m = __builtin_elementwise_maximum(m, v[i]);
+  int nan_cnt = 0;
+  if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
+#pragma unroll
+    for (int i = 0; i < 128; ++i) {
+      const bool isn = __builtin_isnan(v[i]);
+      nan_cnt += isn ? 1 : 0;
+      v[i] = isn ? __builtin_inff() : v[i];
+    }
+  }
+  // sign domains: L=2 (+,-); L=4 (+,-,-,+)
+  const uint32_t sgn0 = (L == 2 ? (h == 1) : (h == 1 || h == 2)) ? 0x80000000u : 0u;
+  const uint32_t odd = (h & 1) ? 0x80000000u : 0u;
+  flip(v, sgn0);
+  sort4_blocks<128>(v);
+  network_plain<128, 128, 0, 128, kNetFrom4>(v);
+  // level 1: pairs (h, h^1)
+  cross_step<1>(v);
+  flip(v, odd);
+  network_plain<128, 128, 0, 128, kNetMerge>(v);
+  if constexpr (L == 4) {
+    // level 2: stride-256 step with h^2, stride-128 step with h^1 (odd lanes flipped around it)
+    cross_step<2>(v);
+    flip(v, odd);
+    cross_step<1>(v);
+    flip(v, odd);
+    network_plain<128, 128, 0, 128, kNetMerge>(v);
+  }
+  // total NaN count of the coordinate
+  if constexpr (L == 2) {
+    nan_cnt += __builtin_bit_cast(int, swap_adjacent(__builtin_bit_cast(float, nan_cnt)));
+  } else {
+    nan_cnt = __builtin_bit_cast(int, from_lane<L, 0>(__builtin_bit_cast(float, nan_cnt))) +
+              __builtin_bit_cast(int, from_lane<L, 1>(__builtin_bit_cast(float, nan_cnt))) +
+              __builtin_bit_cast(int, from_lane<L, 2>(__builtin_bit_cast(float, nan_cnt))) +
+              __builtin_bit_cast(int, from_lane<L, 3>(__builtin_bit_cast(float, nan_cnt)));
+  }
+  float res;
+  if constexpr (MODE == kMedian) {
+    // sorted slots P/2-1 and P/2
+    float zl, zh;
+    if constexpr (L == 2) {
+      zl = from_lane<L, 0>(v[127]);
+      zh = from_lane<L, 1>(v[0]);
+    } else {
+      zl = from_lane<L, 1>(v[127]);
+      zh = -from_lane<L, 3>(v[127]);
+    }
+    res = (n & 1) ? zl : (zl + zh) * 0.5f;
+    if (nan_cnt > 0) res = qnan();
+  } else {
+    // ascending walk over [lo, hi) with one accumulator handed lane to lane
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < 128; ++r)
+      if (r >= lo && r < hi) { if constexpr (!kExactB) asm volatile(""); acc += v[r]; }   // lane 0: slots 0..127
+    acc = from_lane<L, 0>(acc);
+#pragma unroll
+    for (int r = 0; r < 128; ++r)
+      if (128 + r >= lo && 128 + r < hi) { if constexpr (!kExactB) asm volatile(""); acc += v[r]; }   // lane 1
+    acc = from_lane<L, 1>(acc);
+    if constexpr (L == 4) {
+#pragma unroll
+      for (int r = 127; r >= 0; --r)
+        if (383 - r >= lo && 383 - r < hi) { if constexpr (!kExactB) asm volatile(""); acc -= v[r]; }   // lane 3
+      acc = from_lane<L, 3>(acc);
+#pragma unroll
+      for (int r = 127; r >= 0; --r)
+        if (511 - r >= lo && 511 - r < hi) { if constexpr (!kExactB) asm volatile(""); acc -= v[r]; }   // lane 2
+      acc = from_lane<L, 2>(acc);
+    }
+    res = acc / static_cast<float>(hi - lo);
+    if (nan_cnt > n - hi) res = qnan();
+  }
+  if (h == 0 && c < rem) out[base + c] = res;
+}
+
+// ---------------------------------------------------------------------------
 // LDS path for n > 128: a tile of T coordinates x Pn (next_pow2(n)) values,
 // stored [position][coordinate] so that a wave's CE accesses hit 64 distinct
 // banks; bitonic network by the whole workgroup; one lane per coordinate then
@@ -795,6 +977,22 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
       default: break;
     }
 #undef SRA_SEL1
+  }
+  // 128 < N <= 512: 2 or 4 lanes per coordinate, register-resident, DPP merges
+  const bool quad_ok = ldx * 4 * 3 + 256 < (int64_t(1) << 32);   // 32-bit lane offsets
+  if (quad_ok && force != 2 && n > 128 && n <= 256) {
+    hipLaunchKernelGGL((select_quad_kernel<2, MODE>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, ldx, lo, hi, out);
+    return launch_status("select_quad_kernel");
+  }
+  if (quad_ok && n > 256 && n <= 512) {
+    if (n == 512 && (MODE == kMedian || (lo == 51 && hi == 461))) {
+      hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51>), dim3(cdiv(d, 64)), dim3(256),
+                         0, s, X, n, d, ldx, lo, hi, out);
+    } else {
+      hipLaunchKernelGGL((select_quad_kernel<4, MODE>), dim3(cdiv(d, 64)), dim3(256), 0, s, X, n, d, ldx, lo, hi,
+                         out);
+    }
+    return launch_status("select_quad_kernel");
   }
   if (two_lane_ok && n > 128 && n <= 256) {
     hipLaunchKernelGGL((select2_kernel<128, MODE, 0, -1, 256>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, ldx,

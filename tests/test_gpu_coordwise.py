@@ -112,3 +112,25 @@ def test_lds_dma_path_bitexact(n, d, ldx):
         warnings.simplefilter("ignore")
         np.testing.assert_array_equal(engine.trimmed_mean(X).cpu().numpy(), orc.trimmed_mean(list(x)))
         np.testing.assert_array_equal(engine.median(X).cpu().numpy(), orc.median(list(x)))
+
+
+@pytest.mark.parametrize("n", [129, 200, 256, 257, 300, 384, 511, 512])
+def test_multilane_path_bitexact(n):
+    """N in (128, 512]: 2 or 4 lanes per coordinate with DPP bitonic merges
+    (exact N = 512 specialisation and runtime-N padding), NaN / inf / ties."""
+    import warnings
+    rng = np.random.default_rng(n)
+    d = 5000 + n
+    x = make_rows(n, d, seed=3 * n)
+    x[:, :40] = rng.integers(-2, 3, size=(n, 40)).astype(np.float32)     # ties
+    x[rng.integers(0, n, 60), rng.integers(0, d, 60)] = np.inf
+    x[rng.integers(0, n, 60), rng.integers(0, d, 60)] = -np.inf
+    x[rng.integers(0, n, 60), rng.integers(0, d, 60)] = np.nan
+    x[: int(0.1 * n) + 1, 77] = np.nan                                  # NaN survives the trim
+    X = torch.from_numpy(x).cuda()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        np.testing.assert_array_equal(engine.trimmed_mean(X).cpu().numpy(), orc.trimmed_mean(list(x)))
+        np.testing.assert_array_equal(engine.median(X).cpu().numpy(), orc.median(list(x)))
+        for beta in (0.0, 0.3):
+            np.testing.assert_array_equal(engine.trimmed_mean(X, beta).cpu().numpy(), orc.trimmed_mean(list(x), beta))
