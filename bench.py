@@ -126,6 +126,22 @@ KERNEL_NAME = {
     "mom_filterl2": "whole op (bucket means + spectral_filter_kernel<0>)",
     "mom_ex_noregret": "whole op (bucket means + spectral_filter_kernel<1>)",
 }
+
+
+def kernel_label(agg, n):
+    """Name of the dominant kernel for the configuration actually launched."""
+    if agg in ("trimmedmean", "median") and n > 128:
+        mode = 1 if agg == "trimmedmean" else 0
+        if n == 512:
+            return "select_quad_kernel<4, %d, 512, %d>" % (mode, 51 if mode else -1)
+        return "select_quad_kernel<%d, %d>" % (2 if n <= 256 else 4, mode)
+    if agg == "trimmedmean" and n == 100:
+        return "select_plain_kernel<1, 100, 10>"
+    if agg == "median" and n == 100:
+        return "select_reg_kernel<112, 0, 100>"
+    return KERNEL_NAME[agg]
+
+
 MFMA_PEAK_TFLOPS = 157.3      # fp32 MFMA (MI355X_MICROARCH.md)
 MFMA64_PEAK_TFLOPS = 78.6     # fp64 MFMA
 
@@ -309,7 +325,7 @@ def main():
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
                    "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, a.chunks)
                                    if pipelined else "d-shard x%d" % world)},
-        "roofline": {"bound": bound, "kernel": KERNEL_NAME[a.agg], "achieved": round(achieved, 2),
+        "roofline": {"bound": bound, "kernel": kernel_label(a.agg, n), "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic, "kernel_ms": round(kern_ms, 4),
                      ("algorithmic_bytes_per_launch" if unit == "GB/s" else "algorithmic_flops_per_launch"): alg},

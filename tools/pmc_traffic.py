@@ -19,8 +19,10 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"trimmedmean": "select_reg_kernel", "median": "select_reg_kernel", "average": "average",
-            "trimmedmean_n100": "select_reg_kernel", "krum": "gram_partial_kernel"}
+DOMINANT = {"trimmedmean": "select_plain_kernel", "median": "select_reg_kernel", "average": "average",
+            "trimmedmean_n100": "select_plain_kernel", "median_n100": "select_reg_kernel",
+            "trimmedmean_n512": "select_quad_kernel", "median_n512": "select_quad_kernel",
+            "krum": "gram_partial_kernel"}
 
 
 def _find(d, pat):

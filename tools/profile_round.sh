@@ -13,12 +13,19 @@ WORKLOADS=${WORKLOADS:-"trimmedmean|--agg trimmedmean
 median|--agg median
 average|--agg average
 trimmedmean_n100|--agg trimmedmean --clients 100
+median_n100|--agg median --clients 100
+trimmedmean_n512|--agg trimmedmean --clients 512 --d 1.25e7
+median_n512|--agg median --clients 512 --d 1.25e7
 krum|--agg krum --d 1e7
+mom_krum|--agg mom_krum --clients 512 --d 1.25e7
 bulyankrum|--agg bulyankrum --d 1e7
+bulyanmedian|--agg bulyanmedian --d 1e7 --steps 2
 bulyantrimmedmean|--agg bulyantrimmedmean --d 1e7 --steps 2
 filterl2|--agg filterl2 --d 1e7 --steps 2
-ex_noregret|--agg ex_noregret --d 1e7 --steps 2"}
-PMC_WORKLOADS=${PMC_WORKLOADS:-"trimmedmean median average krum"}
+ex_noregret|--agg ex_noregret --d 1e7 --steps 2
+mom_filterl2|--agg mom_filterl2 --clients 512 --d 1.25e7 --steps 2
+mom_ex_noregret|--agg mom_ex_noregret --clients 512 --d 1.25e7 --steps 2"}
+PMC_WORKLOADS=${PMC_WORKLOADS:-"trimmedmean median average trimmedmean_n100 trimmedmean_n512 median_n512 krum"}
 while IFS='|' read -r name args; do
   [[ -z "$name" ]] && continue
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUTD/$name" -o run \
