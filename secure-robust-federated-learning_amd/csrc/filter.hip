@@ -271,20 +271,13 @@ __device__ __forceinline__ int block_min_int(int v, int* ired) {
   return r;
 }
 
-// Sturm count with a Newton-refined reciprocal instead of a full division
-__device__ __forceinline__ int sturm_count_fast(const double* a, const double* b2, int m, double x, double tiny) {
-  int cnt = 0;
-  double dd = a[0] - x;
-  for (int k = 0; k < m; ++k) {
-    if (k > 0) {
-      double r = __builtin_amdgcn_rcp(dd);
-      r = r * (2.0 - dd * r);
-      dd = (a[k] - x) - b2[k - 1] * r;
-    }
-    if (fabs(dd) < tiny) dd = -tiny;
-    if (dd < 0) ++cnt;
-  }
-  return cnt;
+// a / b from the hardware reciprocal with one Newton step and one residual
+// correction (within an ulp or two; the twisted factorisation's pivots only)
+__device__ __forceinline__ double fdiv(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
 }
 
 template <int MODE>  // 0: filterL2, 1: ex_noregret
@@ -568,74 +561,144 @@ __global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
         double tscale = 0.0;
         double theta_lb = -1e300;   // top Ritz value of the previous check
         int next_check = m_hint > 8 ? m_hint : 8;
+        // Lanczos with deferred normalisation (3-4 barriers per step):
+        //   xv = W^1/2 rr, rr = beta_{j-1} q_j when `pend` (q_j not yet stored),
+        //   else rr = q_j.  One operator pass yields M rr, alpha_j and |rr|^2
+        //   together; full re-orthogonalisation by classical Gram-Schmidt with
+        //   a second pass only when the first removed more than half of |r|^2
+        //   (DGKS criterion, |r1|^2 = |r0|^2 - |h|^2).
+        bool pend = false;
+        double rr = own ? V[tid] : 0.0;
+        double r = 0.0;
+        double bprev = 0.0;
         for (int j = 0; j < msteps; ++j) {
-          // r = M q_j - a_j q_j - b_{j-1} q_{j-1}
           if (dbg) t0c = clock64();
-          double r = cmul();
-          if (dbg) { const long long t = clock64(); tm[0] += t - t0c; t0c = t; }
-          const double qv = own ? V[j * VST + tid] : 0.0;
-          r = own ? sw[tid] * r : 0.0;
-          const double aj = block_sum(qv * r, red);
-          if (own) {
-            r -= aj * qv;
-            if (j > 0) r -= beta[j - 1] * V[(j - 1) * VST + tid];
-            rv[tid] = r;
+          // ---- (1) y = G xv with the sums for the centring, alpha and |rr|^2
+          {
+            const double p = gmv_row(xv);
+            double a1 = own ? xv[tid] : 0.0;
+            double a2 = own ? gw[tid] * xv[tid] : 0.0;
+            double a3 = ghalf == 0 ? xv[grow] * p : 0.0;
+            double a4 = own ? rr * rr : 0.0;
+            a1 = wave_sum(a1);
+            a2 = wave_sum(a2);
+            a3 = wave_sum(a3);
+            a4 = wave_sum(a4);
+            if (lane == 0) {
+              red[wave] = a1;
+              red[4 + wave] = a2;
+              red[8 + wave] = a3;
+              red[12 + wave] = a4;
+            }
+            if (ghalf == 0) yv[grow] = p;
           }
-          if (tid == 0) alpha[j] = aj;
+          __syncthreads();
+          if (dbg) { const long long t = clock64(); tm[0] += t - t0c; t0c = t; }
+          // ---- (2) r = M q_j - alpha_j q_j - beta_{j-1} q_{j-1}
+          double aj;
+          {
+            const double s1 = (red[0] + red[1]) + (red[2] + red[3]);
+            const double gy = (red[4] + red[5]) + (red[6] + red[7]);
+            const double xgx = (red[8] + red[9]) + (red[10] + red[11]);
+            const double nrm2 = (red[12] + red[13]) + (red[14] + red[15]);
+            const double bet = pend ? sqrt(nrm2) : 1.0;
+            if (pend) {
+              bprev = bet;
+              if (tid == 0) {
+                beta[j - 1] = bet;
+                beta2[j - 1] = bet * bet;
+              }
+            }
+            aj = (xgx - 2.0 * s1 * gy + scal[0] * s1 * s1) / (bet * bet);
+            tscale = fmax(tscale, fabs(aj) + bprev);
+            if (own) {
+              const double q = rr / bet;
+              if (pend) V[j * VST + tid] = q;
+              r = sw[tid] * (yv[tid] - gw[tid] * s1 - gy + scal[0] * s1) / bet - aj * q;
+              if (j > 0) r -= bprev * V[(j - 1) * VST + tid];
+              rv[tid] = r;
+            }
+          }
           __syncthreads();
           if (dbg) { const long long t = clock64(); tm[1] += t - t0c; t0c = t; }
-          // full re-orthogonalisation against q_0..q_j (classical GS, twice);
-          // dot products: 4 threads per basis vector, 32 entries each
+          // ---- (3) re-orthogonalisation against q_0..q_j
+          double est2 = 0.0;   // |r|^2 after the last pass (Pythagoras)
 #pragma unroll 1
           for (int pass = 0; pass < 2; ++pass) {
             {
-              // 4 lanes per basis vector, entries interleaved (i = part + 4e)
+              // 4 lanes per basis vector, 16-byte chunks interleaved; slot
+              // j+1 is |r|^2 itself
               const int qq = tid >> 2, part = tid & 3;
-              double h0 = 0.0, h1 = 0.0, h2 = 0.0, h3 = 0.0;
-              if (qq <= j) {
-                const double* vq = V + qq * VST + part;
-                const double* rp = rv + part;
+              double h0 = 0.0, h1 = 0.0;
+              if (qq <= j + 1) {
+                const double2* vq = reinterpret_cast<const double2*>(qq <= j ? V + qq * VST : rv) + part;
+                const double2* rp = reinterpret_cast<const double2*>(rv) + part;
 #pragma unroll
-                for (int e = 0; e < 128; e += 16) {
-                  h0 += vq[e] * rp[e];
-                  h1 += vq[e + 4] * rp[e + 4];
-                  h2 += vq[e + 8] * rp[e + 8];
-                  h3 += vq[e + 12] * rp[e + 12];
+                for (int e = 0; e < 64; e += 8) {
+                  const double2 a = vq[e], b = rp[e];
+                  const double2 c2 = vq[e + 4], d2 = rp[e + 4];
+                  h0 += a.x * b.x + a.y * b.y;
+                  h1 += c2.x * d2.x + c2.y * d2.y;
                 }
               }
-              double h = (h0 + h1) + (h2 + h3);
+              double h = h0 + h1;
               h += dpp_f64<0xB1>(h);
               h += dpp_f64<0x4E>(h);
-              if (part == 0 && qq <= j) hq[qq] = h;
+              if (part == 0 && qq <= j + 1) hq[qq] = h;
             }
             __syncthreads();
-            if (own) {
+            double hn2 = 0.0;
+            {
               double u0 = 0.0, u1 = 0.0, u2 = 0.0, u3 = 0.0;
               int qq = 0;
               for (; qq + 3 <= j; qq += 4) {
-                u0 += hq[qq] * V[qq * VST + tid];
-                u1 += hq[qq + 1] * V[(qq + 1) * VST + tid];
-                u2 += hq[qq + 2] * V[(qq + 2) * VST + tid];
-                u3 += hq[qq + 3] * V[(qq + 3) * VST + tid];
+                const double c0 = hq[qq], c1 = hq[qq + 1], c2 = hq[qq + 2], c3 = hq[qq + 3];
+                hn2 += (c0 * c0 + c1 * c1) + (c2 * c2 + c3 * c3);
+                if (own) {
+                  u0 += c0 * V[qq * VST + tid];
+                  u1 += c1 * V[(qq + 1) * VST + tid];
+                  u2 += c2 * V[(qq + 2) * VST + tid];
+                  u3 += c3 * V[(qq + 3) * VST + tid];
+                }
               }
-              for (; qq <= j; ++qq) u0 += hq[qq] * V[qq * VST + tid];
-              r -= (u0 + u1) + (u2 + u3);
-              if (pass == 0) rv[tid] = r;
+              for (; qq <= j; ++qq) {
+                const double c0 = hq[qq];
+                hn2 += c0 * c0;
+                if (own) u0 += c0 * V[qq * VST + tid];
+              }
+              if (own) r -= (u0 + u1) + (u2 + u3);
             }
-            if (pass == 0) __syncthreads();
+            const double r02 = hq[j + 1];
+            est2 = r02 - hn2;
+            if (tid == 0) alpha[j] = pass == 0 ? aj + hq[j] : alpha[j] + hq[j];
+            // DGKS: a second pass only if the first removed over half of |r|^2
+            if (pass == 1 || !(est2 < 0.5 * r02)) break;
+            if (own) rv[tid] = r;
+            __syncthreads();
           }
           if (dbg) { const long long t = clock64(); tm[2] += t - t0c; t0c = t; }
+          m = j + 1;
+          const bool maybe_breakdown = !(est2 > 1e-26 * tscale * tscale);
+          const bool check = m == msteps || maybe_breakdown || m >= next_check;
+          if (!check) {
+            // deferred normalisation: the next step's operator pass measures |r|
+            if (own) {
+              rr = r;
+              xv[tid] = sw[tid] * r;
+            }
+            pend = true;
+            __syncthreads();
+            continue;
+          }
           const double bj = sqrt(block_sum(own ? r * r : 0.0, red));
           if (dbg) { const long long t = clock64(); tm[3] += t - t0c; t0c = t; }
           if (tid == 0) {
             beta[j] = bj;
             beta2[j] = bj * bj;
           }
-          m = j + 1;
-          tscale = fmax(tscale, fabs(aj) + bj + (j > 0 ? beta[j - 1] : 0.0));
           const bool breakdown = !(bj > 1e-14 * tscale);
           const bool last = m == msteps || breakdown;
-          if (last || m >= next_check) {
+          {
             __syncthreads();
             // top eigenpair of T_m (wave 0, T in registers: lane q holds
             // alpha_q, beta_q): multisection on Sturm counts, bracket from the
@@ -645,33 +708,56 @@ __global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
               const double al = lane < m ? alpha[lane] : 0.0;
               const double bl = lane + 1 < m ? beta[lane] : 0.0;
               const double bp = (lane >= 1 && lane < m) ? beta[lane - 1] : 0.0;
-              const double b2l = bl * bl;
               const double rad = fabs(bp) + fabs(bl);
               double lo = wave_min(lane < m ? al - rad : 1e300);
               double hi = wave_max(lane < m ? al + rad : -1e300);
-              if (theta_lb > lo && theta_lb < hi) lo = theta_lb;
               const double tiny = 1e-300 + 1e-30 * tscale;
+              // 64-point multisection on Sturm counts.  The count uses the
+              // division-free three-term recurrence of the leading principal
+              // minors p_q (d_q = p_q / p_{q-1} of the LDL^T pivots, same
+              // tiny-pivot rule), rescaled by exact powers of two every 4
+              // steps, so the dependent chain is one FMA per step.  With a
+              // previous Ritz value (a lower bound, interlacing) the first
+              // round's points are geometric above it, since the top value
+              // has moved little.
+              const bool geo = theta_lb > lo && theta_lb < hi;
+              if (geo) lo = theta_lb;
               for (int round = 0; round < 16; ++round) {
-                const double x = lo + (hi - lo) * (lane + 1) / 65.0;
-                int cntb = 0;
-                double dd = readlane_f64(al, 0) - x;
-                if (fabs(dd) < tiny) dd = -tiny;
-                cntb += dd < 0.0;
+                const double fr = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, lane - 63)
+                                                      : (lane + 1) / 65.0;
+                const double x = lo + (hi - lo) * fr;
+                // alpha / beta^2 come from LDS at wave-uniform addresses (off
+                // the dependent chain); a zero minor keeps its sign bit (no
+                // division, so no tiny-pivot substitution is needed)
+                double p2 = 1.0;
+                double p1 = alpha[0] - x;
+                int cntb = __builtin_signbit(p1) ? 1 : 0;
+#pragma unroll 4
                 for (int q = 1; q < m; ++q) {
-                  double rc = __builtin_amdgcn_rcp(dd);
-                  rc = rc * (2.0 - dd * rc);
-                  dd = (readlane_f64(al, q) - x) - readlane_f64(b2l, q - 1) * rc;
-                  if (fabs(dd) < tiny) dd = -tiny;
-                  cntb += dd < 0.0;
+                  const double pk = fma(alpha[q] - x, p1, -(beta2[q - 1] * p2));
+                  cntb += (__builtin_signbit(pk) ? 1 : 0) != (__builtin_signbit(p1) ? 1 : 0);
+                  p2 = p1;
+                  p1 = pk;
+                  if ((q & 3) == 3) {
+                    const int e = __builtin_amdgcn_frexp_exp(p1);
+                    p1 = __builtin_amdgcn_ldexp(p1, -e);
+                    p2 = __builtin_amdgcn_ldexp(p2, -e);
+                  }
                 }
                 const unsigned long long ok = __builtin_amdgcn_ballot_w64(cntb >= m);
                 const int first = ok ? __builtin_ctzll(ok) : 64;
-                const double nlo = lo + (hi - lo) * first / 65.0;
-                const double nhi = first < 64 ? lo + (hi - lo) * (first + 1) / 65.0 : hi;
+                const double flo = first == 0 ? 0.0
+                                              : ((geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 64)
+                                                                     : first / 65.0);
+                const double fhi = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 63)
+                                                       : (first + 1) / 65.0;
+                const double nlo = lo + (hi - lo) * flo;
+                const double nhi = first < 64 ? lo + (hi - lo) * fhi : hi;
                 lo = nlo;
                 hi = nhi;
                 if (hi - lo <= 2e-16 * fmax(fabs(lo), fabs(hi))) break;
               }
+              if (dbg) tm[5] += clock64() - t0c;
               const double lm = 0.5 * (lo + hi);
               // twisted factorisation of T - lm I: forward pivots dp, backward dm
               double dpv = 0.0, dmv = 0.0;
@@ -680,7 +766,7 @@ __global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
                 if (fabs(dp) < tiny) dp = -tiny;
                 dpv = writelane_f64(dp, 0, dpv);
                 for (int q = 1; q < m; ++q) {
-                  dp = (readlane_f64(al, q) - lm) - readlane_f64(b2l, q - 1) / dp;
+                  dp = (alpha[q] - lm) - fdiv(beta2[q - 1], dp);
                   if (fabs(dp) < tiny) dp = -tiny;
                   dpv = writelane_f64(dp, q, dpv);
                 }
@@ -688,7 +774,7 @@ __global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
                 if (fabs(dm) < tiny) dm = -tiny;
                 dmv = writelane_f64(dm, m - 1, dmv);
                 for (int q = m - 2; q >= 0; --q) {
-                  dm = (readlane_f64(al, q) - lm) - readlane_f64(b2l, q) / dm;
+                  dm = (alpha[q] - lm) - fdiv(beta2[q], dm);
                   if (fabs(dm) < tiny) dm = -tiny;
                   dmv = writelane_f64(dm, q, dmv);
                 }
@@ -745,7 +831,10 @@ __global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
             const double qn = r / bj;
             V[(j + 1) * VST + tid] = qn;
             xv[tid] = sw[tid] * qn;
+            rr = qn;
           }
+          pend = false;
+          bprev = bj;
           __syncthreads();
         }
         // Ritz vector
@@ -771,7 +860,7 @@ __global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
           rec[FNP + 3] = rs_used;
           rec[FNP + 4] = nact;
           rec[FNP + 5] = scal[0];
-          for (int q = 0; q < 5; ++q) rec[FNP + 6 + q] = static_cast<double>(tm[q]);
+          for (int q = 0; q < 6; ++q) rec[FNP + 6 + q] = static_cast<double>(tm[q]);
         }
       }
       // ---- early exit (robust_estimator.py:164 / :70) ----

@@ -50,8 +50,8 @@ if len(sys.argv) > 2 and sys.argv[2] == "synthetic":
             rss.append(int(r[131]))
         print("mode", mode, "iters", len(ms), "steps", ms, "restarts", rss)
         print("   resid", [float("%.1e" % recs[i, 130]) for i in range(len(ms))][:10])
-        tsum = recs[:len(ms), 134:139].numpy().sum(0)
-        print("   cycles cmul/aj/reorth/beta/check per step:", (tsum / max(1, sum(ms))).round(0), "total Mcyc", tsum.sum() / 1e6)
+        tsum = recs[:len(ms), 134:140].numpy().sum(0)
+        print("   cycles cmul/aj/reorth/beta/check(multisection part) per step:", (tsum / max(1, sum(ms))).round(0), "total Mcyc", tsum[:5].sum() / 1e6)
         torch.cuda.synchronize()
         import time
         t0 = time.perf_counter()
