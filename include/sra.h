@@ -205,6 +205,42 @@ int sra_clipped_mean_f32(const float* M, int64_t k, int64_t d, int64_t ldm, cons
 int sra_clipped_mean_f64(const double* M, int64_t k, int64_t d, int64_t ldm, const double* prev, const double* scale,
                          double* clipped, int64_t ldc, double* out, void* stream);
 
+/* ---- k8: attack-side callers of the path (src/attack.py) ---- */
+
+/* attack_krum (attack.py:202-262) for one layer: X holds the layer of ALL m
+ * clients (row-major, ldx); mal_mask[m] (device, 1 = malicious) and
+ * benign_rows[nbenign] (device, ascending) describe mal_index.  Writes the
+ * malicious layer value -lambda * sign(sum of benign rows) (fp64, d), lambda
+ * (device scalar) and krum's pick at that lambda.  lambda runs 1, 1/2, ... to the
+ * first value below lower_bound, like the reference loop (upper_bound is
+ * overwritten to 1.0 there, :237). */
+int sra_attack_krum_workspace_bytes(int64_t m, int64_t d, double lower_bound, size_t* bytes);
+int sra_attack_krum_f32(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
+                        const int32_t* benign_rows, int32_t nbenign, double lower_bound, double* mal_row,
+                        double* lam_out, int32_t* chosen_out, void* ws, size_t ws_bytes, void* stream);
+
+/* Python's `random` stream (MT19937, genrand_uint32) on the device: state_in =
+ * random.getstate()[1] as 625 uint32 (624 words + position); writes the nwords
+ * tempered outputs and the advanced state (random.setstate continues from it).
+ * Replaces the per-element random.uniform draws of attack_trimmedmean
+ * (attack.py:184-194). */
+int sra_mt19937_words(const uint32_t* state_in, int64_t nwords, uint32_t* words, uint32_t* state_out,
+                      void* stream);
+
+/* attack_trimmedmean (attack.py:157-198) over all D parameters: X = all
+ * clients' updates (row-major, ldx), benign_rows (device), params = the
+ * network's current parameters (D, fp32), words = 2*D outputs of
+ * sra_mt19937_words.  Writes the malicious clients' update (fp64, D). */
+int sra_attack_trimmedmean_f32(const float* X, int64_t D, int64_t ldx, const int32_t* benign_rows, int32_t nbenign,
+                               const float* params, const uint32_t* words, double b, double* mal_row, void* stream);
+
+/* attack_xie (attack.py:362-372) for one layer: out = (-weight * sum of rows[])
+ * / nchoices in the input precision, rows = the benign chosen clients. */
+int sra_attack_xie_f32(const float* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows, double weight,
+                       int64_t nchoices, float* out, void* stream);
+int sra_attack_xie_f64(const double* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows, double weight,
+                       int64_t nchoices, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
