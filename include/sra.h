@@ -241,6 +241,34 @@ int sra_attack_xie_f32(const float* X, int64_t d, int64_t ldx, const int32_t* ro
 int sra_attack_xie_f64(const double* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows, double weight,
                        int64_t nchoices, double* out, void* stream);
 
+/* ---- k9: device-resident client-update store ----
+ * The step either side of the aggregation in simulate.py's round loop.  A
+ * parameter table describes the network: ptrs[nseg] = device addresses of the
+ * contiguous float32 parameter tensors (a device array of uint64), seg[nseg+1]
+ * = their offsets in the flat index space (device int64, seg[0] = 0,
+ * seg[nseg] = D).  One launch covers the whole network. */
+
+/* flat = concat(params): params_copy (simulate.py:146-148). */
+int sra_params_flatten_f32(const uint64_t* ptrs, const int64_t* seg, int32_t nseg, int64_t D, float* flat,
+                           void* stream);
+/* row = snapshot - params in fp32 (simulate.py:193-194, numpy's float32 minus
+ * after the per-layer D2H), then params = snapshot (the restore, :196-199). */
+int sra_record_delta_f32(const uint64_t* ptrs, const int64_t* seg, int32_t nseg, int64_t D, const float* snapshot,
+                         float* row, void* stream);
+/* Momentum form (simulate.py:190-191, iclr2022_bucketing / icml2021_history):
+ * row = (double) fl32(one_minus_beta * fl32(snapshot - params)) + beta * row,
+ * one_minus_beta = float32(1 - beta) as numpy casts the Python scalar; then
+ * params = snapshot. */
+int sra_record_momentum_f64(const uint64_t* ptrs, const int64_t* seg, int32_t nseg, int64_t D,
+                            const float* snapshot, float one_minus_beta, double beta, double* row, void* stream);
+/* params -= agg (simulate.py:400-404): float32 minus for an f32 aggregate; an
+ * f64 aggregate is subtracted in fp64 and rounded once to fp32 (torch's
+ * p.data.sub_(float64 tensor)). */
+int sra_apply_update_f32(const uint64_t* ptrs, const int64_t* seg, int32_t nseg, int64_t D, const float* agg,
+                         void* stream);
+int sra_apply_update_f64(const uint64_t* ptrs, const int64_t* seg, int32_t nseg, int64_t D, const double* agg,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,6 +90,11 @@ _SIGS = {
     "sra_attack_trimmedmean_f32": [_ptr, _i64, _i64, _ptr, _i32, _ptr, _ptr, _dbl, _ptr, _ptr],
     "sra_attack_xie_f32": [_ptr, _i64, _i64, _ptr, _i32, _dbl, _i64, _ptr, _ptr],
     "sra_attack_xie_f64": [_ptr, _i64, _i64, _ptr, _i32, _dbl, _i64, _ptr, _ptr],
+    "sra_params_flatten_f32": [_ptr, _ptr, _i32, _i64, _ptr, _ptr],
+    "sra_record_delta_f32": [_ptr, _ptr, _i32, _i64, _ptr, _ptr, _ptr],
+    "sra_record_momentum_f64": [_ptr, _ptr, _i32, _i64, _ptr, ctypes.c_float, _dbl, _ptr, _ptr],
+    "sra_apply_update_f32": [_ptr, _ptr, _i32, _i64, _ptr, _ptr],
+    "sra_apply_update_f64": [_ptr, _ptr, _i32, _i64, _ptr, _ptr],
 }
 _RESTYPES = {"sra_last_error": ctypes.c_char_p}
 

@@ -101,6 +101,12 @@ def _device():
 def stage_round(local_grads, choices, dtype=torch.float32):
     """Stack ``local_grads[c][l]`` for c in ``choices`` into (N, D) on the device."""
     choices = [int(c) for c in choices]
+    store = getattr(local_grads, "store", None)
+    if store is not None and store.intact(choices):
+        # device-resident local_grads (store.py): one gather of the chosen rows
+        ldt = np.float64 if store.dtype == torch.float64 else np.float32
+        return StagedRound(store.stage(choices, dtype), list(store.seg), list(store.shapes),
+                           [np.dtype(ldt)] * len(store.shapes), True)
     first = local_grads[choices[0]]
     device_io = isinstance(first[0], torch.Tensor) and first[0].is_cuda
     shapes = [tuple(t.shape) for t in first]
@@ -205,6 +211,10 @@ def _device_round(agg, st, args, state, local_grads, choices):
 
 def _write_back(local_grads, choices, st, clipped):
     """simulate.py:380 stores the clipped float64 rows into local_grads."""
+    store = getattr(local_grads, "store", None)
+    if store is not None and store.intact(choices):
+        store.store_rows([int(c) for c in choices], clipped)
+        return
     if st.device_io:
         for i, c in enumerate(choices):
             for l in range(st.nlayers):
@@ -267,10 +277,9 @@ def apply_update(params, average_grad):
             p.data.sub_(g.to(p.device))
 
 
-def aggregate_and_apply(agg, params, local_grads, choices, args, state=None):
-    """Device-resident round: aggregate and subtract from ``params`` without the
-    aggregate leaving the GPU (Krum's pick is gathered on the device too).
-    Returns the per-layer device aggregates."""
+def aggregate_flat(agg, local_grads, choices, args, state=None):
+    """One round's aggregate as a flat (D,) device vector over all layers
+    (Krum's per-layer picks gathered on the device); nothing leaves the GPU."""
     st = _prepare(agg, local_grads, choices, state)
     flat, picks = _device_round(agg, st, args, state, local_grads, choices)
     if picks is not None:
@@ -278,6 +287,19 @@ def aggregate_and_apply(agg, params, local_grads, choices, args, state=None):
         for l in range(st.nlayers):
             lo, hi = st.seg[l], st.seg[l + 1]
             engine.gather_rows(st.cols(l), picks[l:l + 1], out=flat[lo:hi].view(1, hi - lo))
+    return flat, st
+
+
+def aggregate_and_apply(agg, params, local_grads, choices, args, state=None):
+    """Device-resident round: aggregate and subtract from ``params`` without the
+    aggregate leaving the GPU (Krum's pick is gathered on the device too).
+    Returns the per-layer device aggregates."""
+    flat, st = aggregate_flat(agg, local_grads, choices, args, state)
+    store = getattr(local_grads, "store", None)
     views = [flat[st.seg[l]:st.seg[l + 1]].view(st.shapes[l]) for l in range(st.nlayers)]
-    apply_update(params, views)
+    params = list(params)
+    if store is not None and len(params) == len(store.params) and all(a is b for a, b in zip(params, store.params)):
+        store.apply(flat)          # one launch over the whole network (csrc/store.hip)
+    else:
+        apply_update(params, views)
     return views

@@ -20,7 +20,7 @@ run() {  # name timeout cmd...
 }
 
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
   rc=$?
   if [[ $rc -gt 1 ]]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
 fi
