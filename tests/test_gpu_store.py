@@ -262,3 +262,24 @@ def test_fl_round_matches_host_flow(agg, attack):
         if momentum:
             for c in choices:
                 np.testing.assert_allclose(_flat(S.local_grads[c]), _flat(host_lg[c]), rtol=0, atol=1e-12)
+
+
+def test_gan_layers_from_store_byte_identical(tmp_path):
+    """formats.save_gan_layers on store-backed local_grads (one device gather +
+    one copy per layer) writes the same bytes as the reference's np.save of the
+    host list (simulate_gan.py:306-313)."""
+    import io
+    from srfl_amd import formats, store as st
+    params = _params(CONVNET, 9)
+    S = st.ClientStore(params, nworker=6)
+    S.snapshot()
+    for c in range(6):
+        _perturb(params, 30 + c)
+        S.record(c)
+    choices = np.array([4, 1, 5, 0])
+    host = [[t.cpu().numpy() for t in S.local_grads[c]] for c in range(6)]
+    for idx, p in enumerate(formats.save_gan_layers(S.local_grads, choices, 2, str(tmp_path))):
+        buf = io.BytesIO()
+        np.save(buf, [host[c][idx] for c in choices])
+        with open(p, "rb") as f:
+            assert f.read() == buf.getvalue()
