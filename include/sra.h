@@ -269,6 +269,34 @@ int sra_apply_update_f32(const uint64_t* ptrs, const int64_t* seg, int32_t nseg,
 int sra_apply_update_f64(const uint64_t* ptrs, const int64_t* seg, int32_t nseg, int64_t D, const double* agg,
                          void* stream);
 
+/* ---- k10: the DBA harness's Helper aggregators (src/DBA/helper.py) ---- */
+
+/* out[j] = s_k of column j (ascending, NaN anywhere -> NaN); k = (n-1)/2 is
+ * torch.median's lower median (Helper.median, helper.py:529-569).  n <= 128. */
+int sra_order_stat_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t k, float* out, void* stream);
+/* out = (sequential fp32 sum of the rows) / divisor, correctly rounded:
+ * Helper.mom_krum's aliased bucket (helper.py:857-863, divisor count + 1) and
+ * Helper.sharding's shard average (helper.py:1155-1164, divisor count). */
+int sra_rows_sum_div_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, float divisor, float* out,
+                         void* stream);
+/* out = sum_r fl32(w[r] * X[r]) accumulated in row order from 0 in fp32, no
+ * FMA (Helper.weighted_average_oracle, helper.py:1199-1221); w: device fp32. */
+int sra_weighted_sum_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, const float* w, float* out,
+                         void* stream);
+/* As sra_clip_scale_f32 with the DBA norm rule (Helper.history / bucketing,
+ * helper.py:753-759, 803-809): norm = sqrt(norm + ||layer_l - prev_l||^2) after
+ * every layer, scale = min(1, tau / norm). */
+int sra_clip_scale_running_f32(const float* M, int64_t k, int64_t d, int64_t ldm, const double* prev,
+                               const int64_t* seg, int32_t nseg, double tau, double* scale, double* norm, void* ws,
+                               size_t ws_bytes, void* stream);
+/* Helper.bulyan_krum / bulyan_median / bulyan_trimmed_mean (helper.py:942-1137):
+ * as sra_bulyan_f32 (same modes, workspace from sra_bulyan_workspace_bytes)
+ * with the DBA selection rules -- Krum rounds count the zero self-distance
+ * (= Krum with f + 1 over the others; f = 1 is rejected), median rounds take
+ * the lower median.  The per-coordinate stage is shared (fp64). */
+int sra_bulyan_dba_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
+                       int32_t* selected, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,6 +95,12 @@ _SIGS = {
     "sra_record_momentum_f64": [_ptr, _ptr, _i32, _i64, _ptr, ctypes.c_float, _dbl, _ptr, _ptr],
     "sra_apply_update_f32": [_ptr, _ptr, _i32, _i64, _ptr, _ptr],
     "sra_apply_update_f64": [_ptr, _ptr, _i32, _i64, _ptr, _ptr],
+    "sra_order_stat_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr],
+    "sra_rows_sum_div_f32": [_ptr, _i64, _i64, _i64, ctypes.c_float, _ptr, _ptr],
+    "sra_weighted_sum_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr, _ptr],
+    "sra_clip_scale_running_f32": [_ptr, _i64, _i64, _i64, _ptr, ctypes.POINTER(_i64), _i32, _dbl, _ptr, _ptr, _ptr,
+                                   _sz, _ptr],
+    "sra_bulyan_dba_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
 }
 _RESTYPES = {"sra_last_error": ctypes.c_char_p}
 

@@ -475,8 +475,12 @@ __global__ void iota_kernel(int* p, int n) {
   if (i < n) p[i] = i;
 }
 
+// dba = true: the DBA harness's Helper.bulyan_* (src/DBA/helper.py:942-1137).  Its Krum rounds keep the
+// zero self-distance among the size - i - f - 2 smallest (:979-980), i.e. Krum with f + 1 over the
+// other clients (identical while remaining - f - 2 >= 1: f >= 2 or f == 0); its median rounds take
+// torch.median's LOWER median (:1025); trimmed-mean rounds and theta / beta are unchanged.
 int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode, double* out, int* sel_out,
-                  void* ws, size_t ws_bytes, hipStream_t s) {
+                  void* ws, size_t ws_bytes, hipStream_t s, bool dba = false) {
   const int theta = n - 2 * f;
   SRA_REQUIRE(theta > 0, SRA_ERR_THETA, "bulyan needs theta = N - 2f > 0 (N=%d, f=%d)", n, f);
   SRA_REQUIRE(mode >= 0 && mode <= 2, SRA_ERR_ARG, "bad bulyan mode %d", mode);
@@ -491,7 +495,7 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   char* rest = p + 4096 + 4 * static_cast<size_t>(n) * 4;
   int rc;
   if (mode == kBulyanKrum) {
-    rc = launch_krum(X, n, d, ldx, f, theta, order, nullptr, rest, krum_workspace_bytes(n, d), s);
+    rc = launch_krum(X, n, d, ldx, dba ? f + 1 : f, theta, order, nullptr, rest, krum_workspace_bytes(n, d), s);
     if (rc) return rc;
     if (sel_out) SRA_HIP(hipMemcpyAsync(sel_out, order, sizeof(int) * theta, hipMemcpyDeviceToDevice, s));
     return launch_final(X, ldx, order, theta, beta, d, out, s);
@@ -511,7 +515,10 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   for (int t = 0; t < theta; ++t) {
     const int nr = n - t;
     float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
-    if (mode == kBulyanMedian) {
+    if (mode == kBulyanMedian && dba) {
+      const int k = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
+      rc = launch_select_rows<1>(X, ldx, cur, nr, d, k, k + 1, agg, s);
+    } else if (mode == kBulyanMedian) {
       rc = launch_select_rows<0>(X, ldx, cur, nr, d, 0, nr, agg, s);
     } else {
       const int b = static_cast<int>(nr * 0.1);  // trimmed_mean(beta=0.1): int(size * beta)
@@ -554,4 +561,14 @@ extern "C" int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx,
   SRA_REQUIRE(n >= 1 && n <= 256 && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= 256)");
   return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
                        static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_bulyan_dba_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode,
+                                  double* out, int32_t* selected, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= 256 && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= 256)");
+  SRA_REQUIRE(!(mode == kBulyanKrum && f == 1), SRA_ERR_ARG,
+              "DBA bulyan_krum with f = 1 (its last round scores an empty neighbour set) is not supported");
+  return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
+                       static_cast<hipStream_t>(stream), true);
 }

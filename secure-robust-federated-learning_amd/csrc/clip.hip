@@ -169,6 +169,22 @@ __global__ void __launch_bounds__(kClipBS) clip_scale_kernel(const double* __res
   if (norm_out != nullptr) norm_out[r] = nrm;
 }
 
+// DBA Helper.history / bucketing (src/DBA/helper.py:753-759, 803-809): the
+// running value is re-rooted after every layer, norm_l = sqrt(norm_{l-1} +
+// ||layer_l||^2) -- not the L2 norm across layers; scale = min(1, tau / norm_L).
+__global__ void __launch_bounds__(kClipBS) clip_scale_running_kernel(const double* __restrict__ segsq, int k,
+                                                                    int nseg, double tau,
+                                                                    double* __restrict__ scale,
+                                                                    double* __restrict__ norm_out) {
+  const int r = blockIdx.x * kClipBS + threadIdx.x;
+  if (r >= k) return;
+  double nrm = 0.0;
+  for (int l = 0; l < nseg; ++l) nrm = __builtin_sqrt(nrm + segsq[static_cast<int64_t>(r) * nseg + l]);
+  const double x = tau / nrm;
+  scale[r] = x < 1.0 ? x : 1.0;
+  if (norm_out != nullptr) norm_out[r] = nrm;
+}
+
 // ---------------------------------------------------------------------------
 // clipped mean
 // ---------------------------------------------------------------------------
@@ -207,7 +223,7 @@ static int64_t seg_tiles(const int64_t* seg, int32_t nseg) {
   return t;
 }
 
-template <typename T>
+template <typename T, bool RUNNING = false>
 static int launch_clip_scale(const T* M, int64_t k, int64_t d, int64_t ldm, const double* prev, const int64_t* seg,
                              int32_t nseg, double tau, double* scale, double* norm_out, void* ws, size_t ws_bytes,
                              void* stream) {
@@ -239,6 +255,11 @@ static int launch_clip_scale(const T* M, int64_t k, int64_t d, int64_t ldm, cons
     int rc = launch_status("sqdist_segment_kernel");
     if (rc) return rc;
     tile0 += nt;
+  }
+  if constexpr (RUNNING) {
+    hipLaunchKernelGGL(clip_scale_running_kernel, dim3(cdiv(k, kClipBS)), dim3(kClipBS), 0, s, segsq, (int)k, nseg,
+                       tau, scale, norm_out);
+    return launch_status("clip_scale_running_kernel");
   }
   hipLaunchKernelGGL(clip_scale_kernel, dim3(cdiv(k, kClipBS)), dim3(kClipBS), 0, s, segsq, (int)k, nseg, tau, scale,
                      norm_out);
@@ -296,4 +317,10 @@ extern "C" int sra_clipped_mean_f32(const float* M, int64_t k, int64_t d, int64_
 extern "C" int sra_clipped_mean_f64(const double* M, int64_t k, int64_t d, int64_t ldm, const double* prev,
                                     const double* scale, double* clipped, int64_t ldc, double* out, void* stream) {
   return launch_clipped_mean<double>(M, k, d, ldm, prev, scale, clipped, ldc, out, stream);
+}
+
+extern "C" int sra_clip_scale_running_f32(const float* M, int64_t k, int64_t d, int64_t ldm, const double* prev,
+                                          const int64_t* seg, int32_t nseg, double tau, double* scale, double* norm,
+                                          void* ws, size_t ws_bytes, void* stream) {
+  return launch_clip_scale<float, true>(M, k, d, ldm, prev, seg, nseg, tau, scale, norm, ws, ws_bytes, stream);
 }

@@ -28,7 +28,7 @@
 
 namespace sra {
 
-enum SelectMode { kMedian = 0, kTrimmed = 1 };
+enum SelectMode { kMedian = 0, kTrimmed = 1, kOrder = 2 };  // kOrder: s[lo], any NaN -> NaN
 
 // ---------------------------------------------------------------------------
 // average: sequential fp32 sum over clients (numpy axis-0 add.reduce order).
@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(BS) select_reg_kernel(const float* __restrict_
   // +inf -- which sorts them last exactly like numpy -- and sorts again.
   network_fast<P2, PR, kOutLo, kOutHi>(v);
   float res = finish(0);
-  if constexpr (MODE != kMedian) {
+  if constexpr (MODE == kTrimmed) {   // (kOrder keeps the propagated NaN: torch.median's answer)
     if (__builtin_amdgcn_ballot_w64(__builtin_isnan(res)) != 0) {
       load_column();
       int nan_cnt = 0;
@@ -1049,4 +1049,32 @@ extern "C" int sra_trimmed_mean_f32(const float* X, int64_t n, int64_t d, int64_
   // numpy slices s[b : n-b]; an empty slice gives mean = NaN (0/0)
   const int lo = b, hi = (int)n - b;
   return launch_select<kTrimmed>(X, (int)n, d, ldx, lo, hi > lo ? hi : lo, out, static_cast<hipStream_t>(stream));
+}
+
+// The k-th order statistic of every column (sorted ascending, NaN anywhere in
+// the column -> NaN).  k = (n-1)/2 is torch.median's lower median, which the
+// DBA harness aggregates with (src/DBA/helper.py:561, :1025).  Runtime-N
+// register network (n <= 128); the kept slot s[k] is summed alone and divided
+// by 1, i.e. returned exactly.
+extern "C" int sra_order_stat_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t k, float* out,
+                                  void* stream) {
+  int rc = check_matrix(X, n, d, ldx, out);
+  if (rc) return rc;
+  SRA_REQUIRE(n <= 128, SRA_ERR_UNSUPPORTED, "order statistic supports N <= 128 (got %lld)", (long long)n);
+  SRA_REQUIRE(k >= 0 && k < n, SRA_ERR_ARG, "order statistic k=%d out of [0, %lld)", k, (long long)n);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int P = static_cast<int>(cdiv(n, 16) * 16);
+  const int64_t blocks = cdiv(d, 256);
+#define SRA_ORD(PP)                                                                                                  \
+  case PP:                                                                                                           \
+    hipLaunchKernelGGL((select_reg_kernel<PP, kOrder, 0, -1, 256>), dim3(blocks), dim3(256), 0, s, X, (int)n, d, ldx, \
+                       (int)k, (int)k + 1, out);                                                                     \
+    return launch_status("select_reg_kernel");
+  switch (P) {
+    SRA_ORD(16) SRA_ORD(32) SRA_ORD(48) SRA_ORD(64) SRA_ORD(80) SRA_ORD(96) SRA_ORD(112) SRA_ORD(128)
+    default: break;
+  }
+#undef SRA_ORD
+  set_error("order statistic: unsupported N %lld", (long long)n);
+  return SRA_ERR_UNSUPPORTED;
 }

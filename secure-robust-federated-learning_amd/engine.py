@@ -292,10 +292,12 @@ def _seg_table(seg, d):
     return arr, len(seg) - 1
 
 
-def clip_scales(M, prev, seg, tau, norms=False):
+def clip_scales(M, prev, seg, tau, norms=False, running=False):
     """scale[r] = min(1, tau / ||M[r] - prev||) with the norm across the layer
     segments ``seg`` (offsets, host ints) as simulate.py:352-356 / 374-378
-    evaluate it.  Returns the (k,) fp64 device tensor (and the norms)."""
+    evaluate it.  Returns the (k,) fp64 device tensor (and the norms).
+    running=True: the DBA harness's rule instead, norm = sqrt(norm + ||layer||^2)
+    after every layer (src/DBA/helper.py:753-759)."""
     M, k, d, ldm = as_rows(M)
     prev = prev.reshape(-1)
     if prev.dtype != torch.float64 or prev.numel() != d or not prev.is_contiguous():
@@ -305,7 +307,10 @@ def clip_scales(M, prev, seg, tau, norms=False):
     ws = _workspace(nb, M.device)
     scale = torch.empty(k, dtype=torch.float64, device=M.device)
     nrm = torch.empty(k, dtype=torch.float64, device=M.device) if norms else None
-    _lib.call("sra_clip_scale_" + _SUFFIX[M.dtype], M.data_ptr(), k, d, ldm, prev.data_ptr(), arr, nseg, float(tau),
+    if running and M.dtype != torch.float32:
+        raise TypeError("the running-norm (DBA) clip rule takes float32 rows")
+    fn = "sra_clip_scale_running_f32" if running else "sra_clip_scale_" + _SUFFIX[M.dtype]
+    _lib.call(fn, M.data_ptr(), k, d, ldm, prev.data_ptr(), arr, nseg, float(tau),
               scale.data_ptr(), nrm.data_ptr() if nrm is not None else None, ws.data_ptr(), nb,
               _stream_ptr(M.device))
     return (scale, nrm) if norms else scale
@@ -341,3 +346,51 @@ def history(X, prev, seg, tau, clipped=None):
     """icml2021_history (simulate.py:374-386): clip every row against prev by
     its cross-layer norm (written to ``clipped`` when given), mean over rows."""
     return clipped_mean(X, prev, clip_scales(X, prev, seg, tau), clipped=clipped)
+
+
+# ---------------------------------------------------------------------------
+# DBA harness primitives (k10, src/DBA/helper.py; SURVEY.md §8(f).4)
+# ---------------------------------------------------------------------------
+def order_stat(X, k, out=None):
+    """s_k of every column (ascending; a NaN anywhere gives NaN).  k = (N-1)//2
+    is torch.median's lower median (helper.py:561)."""
+    X, n, d, ldx = as_matrix(X)
+    out = _out(X, d, out)
+    _lib.call("sra_order_stat_f32", X.data_ptr(), n, d, ldx, int(k), out.data_ptr(), _stream_ptr(X.device))
+    return out
+
+
+def rows_sum_div(X, divisor, out=None):
+    """(sequential fp32 sum of the rows of X) / divisor, torch's in-place
+    ``+=`` then ``/=`` rounding (helper.py:859-863, 1157-1163)."""
+    X, n, d, ldx = as_matrix(X)
+    out = _out(X, d, out)
+    _lib.call("sra_rows_sum_div_f32", X.data_ptr(), n, d, ldx, float(divisor), out.data_ptr(), _stream_ptr(X.device))
+    return out
+
+
+def weighted_sum(X, w, out=None):
+    """sum_r fl32(w[r] * X[r]) accumulated in row order (helper.py:1212-1219);
+    ``w`` a device float32 vector of N weights."""
+    X, n, d, ldx = as_matrix(X)
+    if w.dtype != torch.float32 or w.numel() != n or not w.is_cuda:
+        raise ValueError("w must be a device float32 vector of N weights")
+    w = w.contiguous()
+    out = _out(X, d, out)
+    _lib.call("sra_weighted_sum_f32", X.data_ptr(), n, d, ldx, w.data_ptr(), out.data_ptr(), _stream_ptr(X.device))
+    return out
+
+
+def bulyan_dba(X, f, aggsubfunc="trimmedmean", selected=False):
+    """Helper.bulyan_krum / bulyan_median / bulyan_trimmed_mean selection rules
+    (helper.py:942-1137) with the shared per-coordinate stage; float64 (d,)."""
+    X, n, d, ldx = as_matrix(X)
+    mode = BULYAN_MODES[aggsubfunc]
+    theta = n - 2 * int(f)
+    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    sel = torch.empty(max(theta, 1), dtype=torch.int32, device=X.device) if selected else None
+    nb = _lib.query_bytes("sra_bulyan_workspace_bytes", n, d, int(f), mode)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_bulyan_dba_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
+              sel.data_ptr() if sel is not None else None, ws.data_ptr(), nb, _stream_ptr(X.device))
+    return (out, sel) if selected else out

@@ -48,3 +48,14 @@ def test_missing_library_fails_loudly(tmp_path):
 
 def test_package_version():
     assert srfl_amd.__version__
+
+
+def test_dba_module_needs_a_gpu():
+    import numpy as np
+    import torch
+    from srfl_amd import dba
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = dba.HelperAggregation({"eta": 1})
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        h.median(None, {0: (10, {"w": torch.from_numpy(np.zeros(3, np.float32))})})
