@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--agg", default="trimmedmean",
                     choices=["trimmedmean", "median", "average", "krum", "mom_krum", "bulyankrum", "bulyanmedian",
-                             "bulyantrimmedmean", "filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"])
+                             "bulyantrimmedmean", "filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret",
+                             "dba_median", "dba_weighted_sum"])
     ap.add_argument("--clients", type=int, default=128)
     ap.add_argument("--d", type=float, default=1e8, help="coordinates per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -95,7 +96,21 @@ def _filter_step(fn, mom=False):
     return step
 
 
+_WEIGHTS = {}
+
+
+def _dba_weighted_step(X, out):
+    """DBA Helper.weighted_average_oracle (geometric median's inner step)."""
+    n = int(X.shape[0])
+    w = _WEIGHTS.get(n)
+    if w is None:
+        w = _WEIGHTS[n] = torch.full((n,), 1.0 / n, dtype=torch.float32, device=X.device)
+    engine.weighted_sum(X, w, out=out)
+
+
 AGG = {
+    "dba_median": lambda X, out: engine.order_stat(X, (int(X.shape[0]) - 1) // 2, out=out),
+    "dba_weighted_sum": _dba_weighted_step,
     "trimmedmean": lambda X, out: engine.trimmed_mean(X, 0.1, out=out),
     "median": lambda X, out: engine.median(X, out=out),
     "average": lambda X, out: engine.average(X, out=out),
@@ -113,6 +128,8 @@ OUT_DTYPE = {"bulyankrum": torch.float64, "bulyanmedian": torch.float64, "bulyan
              "filterl2": torch.float64, "ex_noregret": torch.float64, "mom_filterl2": torch.float64,
              "mom_ex_noregret": torch.float64}
 KERNEL_NAME = {
+    "dba_median": "select_reg_kernel<128, kOrder> (lower median, DBA Helper.median)",
+    "dba_weighted_sum": "rows_vec4_kernel<true> (DBA weighted_average_oracle)",
     "trimmedmean": "select_plain_kernel<1, 128, 12>",
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
@@ -148,7 +165,7 @@ MFMA64_PEAK_TFLOPS = 78.6     # fp64 MFMA
 
 def roofline_model(agg, n, d):
     """(bound, peak, unit, algorithmic amount per launch) — SURVEY.md §8(d)."""
-    if agg in ("trimmedmean", "median", "average"):
+    if agg in ("trimmedmean", "median", "average", "dba_median", "dba_weighted_sum"):
         return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
     if agg in ("krum", "mom_krum", "bulyankrum"):
         m = n if agg != "mom_krum" else -(-n // 3)
@@ -165,8 +182,17 @@ def roofline_model(agg, n, d):
 def cpu_baseline(agg, n, budget_s):
     """Time the oracle's CPU port on a bounded sample until ~budget_s elapsed."""
     from oracle import robust_np as orc
+    from oracle import dba_np as odba
     fa = FILTER_ARGS
-    fn = {"trimmedmean": orc.trimmed_mean, "median": orc.median, "average": orc.average,
+
+    def _wsum(xs):
+        acc = np.zeros(xs[0].shape[0], np.float32)
+        w = np.float32(1.0 / len(xs))
+        for r in xs:
+            acc = acc + w * r
+        return acc
+    fn = {"dba_median": lambda xs: odba.median(np.asarray(xs)), "dba_weighted_sum": _wsum,
+          "trimmedmean": orc.trimmed_mean, "median": orc.median, "average": orc.average,
           "krum": lambda xs: orc.krum(xs, 20), "mom_krum": lambda xs: orc.mom_krum(xs, 20),
           "bulyankrum": lambda xs: orc.bulyan(xs, 20, "krum"),
           "bulyanmedian": lambda xs: orc.bulyan(xs, 20, "median"),
@@ -198,7 +224,7 @@ def cpu_baseline(agg, n, budget_s):
                 break
     gbs = reps * n * d * 4 / el / 1e9
     return {"value": round(gbs, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "%d x numpy %s over N=%d x d=%d fp32 (oracle/robust_np.py), %.1f s on host cores, "
+            "sample": "%d x numpy %s over N=%d x d=%d fp32 (oracle/), %.1f s on host cores, "
                       "single thread" % (reps, agg, n, d, el)}
 
 
