@@ -262,3 +262,45 @@ def geometric_median(X, ns, seg, maxiter=4, eps=1e-5, ftol=1e-6):
 
 def update_norm(v):
     return math.sqrt(float(np.sum(np.asarray(v, dtype=np.float64) ** 2)))
+
+
+def foolsgold_weights(grads):
+    """FoolsGold.foolsgold (helper.py:1388-1417): cosine similarity of the client
+    features (sklearn: rows scaled to unit L2 norm, zero rows left as they are),
+    pardoning, clip, rescale, logit.  Returns (wv, alpha) -- the values the
+    reference holds when its ``return wv,alpha(base)`` raises NameError."""
+    g = np.asarray(grads, dtype=np.float64)
+    n = g.shape[0]
+    nrm = np.sqrt(np.einsum("ij,ij->i", g, g))
+    nrm[nrm == 0.0] = 1.0
+    u = g / nrm[:, None]
+    cs = u @ u.T - np.eye(n)
+    maxcs = np.max(cs, axis=1)
+    for i in range(n):
+        for j in range(n):
+            if i != j and maxcs[i] < maxcs[j]:
+                cs[i][j] = cs[i][j] * maxcs[i] / maxcs[j]
+    wv = 1 - np.max(cs, axis=1)
+    wv[wv > 1] = 1
+    wv[wv < 0] = 0
+    alpha = np.max(cs, axis=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        wv = wv / np.max(wv)
+        wv[(wv == 1)] = .99
+        wv = np.log(wv / (1 - wv)) + 0.5
+    wv[(np.isinf(wv) + wv > 1)] = 1
+    wv[(wv < 0)] = 0
+    return wv, alpha
+
+
+def foolsgold_features(X, seg, memory, names, use_memory):
+    """FoolsGold.aggregate_gradients (helper.py:1328-1345): the second-to-last
+    layer of every client in fp64, accumulated per client name into ``memory``
+    (a dict, updated in place); returns the matrix FoolsGold weighs."""
+    lo, hi = int(seg[-3]), int(seg[-2])
+    grads = X[:, lo:hi].astype(np.float64)
+    mem = np.zeros_like(grads)
+    for i, nm in enumerate(names):
+        memory[nm] = memory[nm] + grads[i] if nm in memory else grads[i].copy()
+        mem[i] = memory[nm]
+    return mem if use_memory else grads

@@ -23,9 +23,11 @@ method names, signatures, return values and exceptions; ``updates`` is the
 ``{name: (num_samples, {layer: tensor})}`` dict of DBA/main.py:181.  Client
 updates are stacked once into a client-major (N, D) float32 matrix on the HIP
 device; every reduction over clients runs in libsra.  There is no CPU
-fallback.  ``foolsgold_update`` (FoolsGold's cosine-similarity weighting over
-accumulated client history, helper.py:291-325, 1321+) is not part of the
-robust-reduction path and is not provided.
+fallback.  ``foolsgold_update`` keeps the reference's behaviour exactly: its
+FoolsGold weighting (helper.py:1388-1417) ends in ``return wv,alpha(base)``,
+which raises NameError on every call, so the weights are computed on the
+device (``foolsgold_weights``, kept on ``self.fg.last``) and the same NameError
+is raised; the model is never updated, as in the reference.
 """
 from __future__ import annotations
 
@@ -76,6 +78,43 @@ class _Staged:
         return {k: vec[self.seg[l]:self.seg[l + 1]].reshape(self.shapes[l]) for l, k in enumerate(self.keys)}
 
 
+class FoolsGoldState:
+    """The FoolsGold object of helper.py:1321-1326 (per-client feature memory)."""
+
+    def __init__(self, use_memory=False):
+        self.memory = None
+        self.memory_dict = dict()
+        self.wv_history = []
+        self.use_memory = use_memory
+        self.last = None
+
+
+def foolsgold_weights(F):
+    """FoolsGold.foolsgold (helper.py:1388-1417) on a device float64 (N, k)
+    feature matrix: cosine similarity (rows at unit L2 norm, zero rows kept;
+    sklearn's cosine_similarity) minus the identity, pardoning
+    cs[i][j] *= maxcs[i] / maxcs[j] where maxcs[i] < maxcs[j], then the
+    clip / rescale / logit of the weights.  Returns (wv, alpha) on the device."""
+    n = int(F.shape[0])
+    eye = torch.eye(n, dtype=torch.float64, device=F.device)
+    nrm = torch.sqrt((F * F).sum(dim=1))
+    nrm = torch.where(nrm == 0, torch.ones_like(nrm), nrm)
+    U = F / nrm[:, None]
+    cs = U @ U.T - eye
+    maxcs = cs.max(dim=1).values
+    pard = (maxcs[:, None] < maxcs[None, :]) & (eye == 0)
+    cs = torch.where(pard, cs * maxcs[:, None] / maxcs[None, :], cs)
+    top = cs.max(dim=1).values
+    wv = (1 - top).clamp(min=0, max=1)
+    alpha = top
+    wv = wv / wv.max()
+    wv = torch.where(wv == 1, torch.full_like(wv, .99), wv)
+    wv = torch.log(wv / (1 - wv)) + 0.5
+    wv = torch.where(torch.isinf(wv).double() + wv > 1, torch.ones_like(wv), wv)
+    wv = torch.where(wv < 0, torch.zeros_like(wv), wv)
+    return wv, alpha
+
+
 class HelperAggregation:
     """The aggregation methods of src/DBA/helper.py ``Helper`` on the engine."""
 
@@ -87,6 +126,7 @@ class HelperAggregation:
         self.params.setdefault("diff_privacy", False)
         self.history_prev_average_grad = None
         self.history_tau = 10.
+        self.fg = FoolsGoldState(use_memory=self.params.get("fg_use_memory", False))
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -324,6 +364,36 @@ class HelperAggregation:
         return num_oracle_calls, is_updated, names, wv.cpu().numpy().tolist(), dist_out
 
 
+def _foolsgold_update(self, target_model, updates):
+    """helper.py:291-325: updates carry per-layer gradient lists; FoolsGold
+    weighs the clients by the second-to-last layer (accumulated per client
+    name when fg.use_memory), helper.py:1328-1345.  The reference's weighting
+    returns through ``alpha(base)`` (:1417) and raises NameError, so this does
+    too, after the same side effects (model in train mode, grads cleared,
+    memory accumulated); the computed (wv, alpha) stay on ``self.fg.last``."""
+    names, _, client_grads = self._collect(updates)
+    if hasattr(target_model, "train"):
+        target_model.train()
+    if hasattr(target_model, "parameters"):
+        for p in target_model.parameters():
+            p.grad = None
+    dev = _device()
+    F = torch.stack([torch.as_tensor(g[-2]).reshape(-1).to(dev, torch.float64) for g in client_grads])
+    mem = []
+    for i, nm in enumerate(names):
+        if nm in self.fg.memory_dict:
+            self.fg.memory_dict[nm] += F[i]
+        else:
+            self.fg.memory_dict[nm] = F[i].clone()
+        mem.append(self.fg.memory_dict[nm])
+    self.fg.memory = torch.stack(mem)
+    self.fg.last = foolsgold_weights(self.fg.memory if self.fg.use_memory else F)
+    raise NameError("name 'base' is not defined")
+
+
+HelperAggregation.foolsgold_update = _foolsgold_update
+
+
 # DBA/main.py:184-240 -- config.AGGR_* name -> call
 def aggregate(helper, method, target_model, updates):
     """Mirror of the if/elif chain of src/DBA/main.py:184-240 (config names of
@@ -357,5 +427,5 @@ def aggregate(helper, method, target_model, updates):
     if method == "bucketing":
         return helper.bucketing(target_model, updates)
     if method == "foolsgold":
-        raise NotImplementedError("foolsgold is outside the robust-reduction path (DESIGN.md, out of scope)")
+        return helper.foolsgold_update(target_model, updates)
     raise ValueError("unknown aggregation method %r" % (method,))

@@ -47,10 +47,14 @@ CASES = {
     "median_sharded_n100": ("median", {}, 100, 20, {"sharding": True}, 1),
     "bucketing_n100": ("bucketing", {}, 100, 20, {}, 2),
     "sharding_n25": ("fed_avg", {}, 25, 5, {"sharding": True}, 1),   # 50 shards of 1 > 25 clients: IndexError
+    # FoolsGold (helper.py:291-325, 1321-1417): updates carry per-layer gradient LISTS; SGD step on the model
+    "foolsgold_n24": ("foolsgold_update", {}, 24, 5, {"fg_use_memory": False}, 2),
+    "foolsgold_mem_n24": ("foolsgold_update", {}, 24, 5, {"fg_use_memory": True}, 2),
 }
 
 BASE_PARAMS = {"eta": 1, "sharding": False, "shard_size": 0.2, "adversary_list": [0, 1, 2, 3, 4],
-               "poisoning_per_batch": 20, "batch_size": 64, "diff_privacy": False}
+               "poisoning_per_batch": 20, "batch_size": 64, "diff_privacy": False,
+               "lr": 0.1, "momentum": 0.9, "decay": 0.0005}
 
 
 def case_rows(name, rnd=0):

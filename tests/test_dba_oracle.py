@@ -125,3 +125,18 @@ def test_geometric_median():
     assert calls == int(f["calls_0"])
     np.testing.assert_allclose(wv, f["wv_0"], rtol=1e-5)
     np.testing.assert_allclose(dist, f["dist_0"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["foolsgold_n24", "foolsgold_mem_n24"])
+def test_foolsgold_weights(name):
+    f = fx(name)
+    memory = {}
+    for rnd in range(2):
+        assert str(f["error_%d" % rnd]) == "NameError"   # helper.py:1417 ``alpha(base)``
+        x, _ = case_rows(name, rnd)
+        g = od.foolsgold_features(x, SEG, memory, list(range(x.shape[0])), case_params(name)["fg_use_memory"])
+        np.testing.assert_allclose(np.array([memory[i] for i in range(x.shape[0])]), f["memory_%d" % rnd],
+                                   rtol=1e-15)
+        wv, alpha = od.foolsgold_weights(g)
+        np.testing.assert_allclose(wv, f["wv_%d" % rnd], rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(alpha, f["alpha_%d" % rnd], rtol=1e-12, atol=1e-14)

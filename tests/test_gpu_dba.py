@@ -176,8 +176,23 @@ def test_dispatch_names():
     m = _Model()
     assert dba.aggregate(h, "median", m, _updates(x, ns)) is True
     np.testing.assert_array_equal(_flat(m.state_dict()).astype(np.float32), fx("median_n24")["out_0"])
-    with pytest.raises(NotImplementedError):
-        dba.aggregate(h, "foolsgold", m, _updates(x, ns))
+    with pytest.raises(NameError):   # the reference's helper.py:1417 raises on every call
+        dba.aggregate(h, "foolsgold", m, {i: (c, list(d.values())) for i, (c, d) in _updates(x, ns).items()})
+
+
+@pytest.mark.parametrize("name", ["foolsgold_n24", "foolsgold_mem_n24"])
+def test_foolsgold(name):
+    f = fx(name)
+    h = dba.HelperAggregation(case_params(name))
+    for rnd in range(2):
+        x, ns = case_rows(name, rnd)
+        ups = {i: (c, [d[k] for k, _ in DBA_LAYERS]) for i, (c, d) in _updates(x, ns).items()}
+        with pytest.raises(NameError):
+            h.foolsgold_update(_Model(), ups)
+        wv, alpha = h.fg.last
+        np.testing.assert_allclose(h.fg.memory.cpu().numpy(), f["memory_%d" % rnd], rtol=1e-15)
+        np.testing.assert_allclose(wv.cpu().numpy(), f["wv_%d" % rnd], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(alpha.cpu().numpy(), f["alpha_%d" % rnd], rtol=1e-9, atol=1e-12)
 
 
 # ------------------------------------------------------------- k10 kernels
