@@ -139,9 +139,25 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
                    int32_t* selected, void* ws, size_t ws_bytes, void* stream);
 
 
+/* The per-coordinate Bulyan stage on float64 values, any input order:
+ * robust_estimator.bulyan_median (src/robust_estimator.py:259-270) and
+ * bulyan_one_coordinate (:272-275) for every column of the theta x d matrix A
+ * (row i = the i-th selected value, row stride lda).  median_index[j]
+ * (optional) = np.argmin of the pairwise-summed distance rows (first NaN if
+ * any); median_row (optional, theta x d, row stride ldr) = that distance row;
+ * out[j] = mean of arr[argsort(row)[:beta]] (Python slice semantics; equal
+ * distances take the smaller value first).  1 <= theta <= 512. */
+int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t d, int64_t lda, int32_t beta, double* out,
+                              int64_t* median_index, double* median_row, int64_t ldr, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Spectral filters (k6)                                                     */
 /* ------------------------------------------------------------------------ */
+
+/* Workspace for sra_filter_f32 / sra_filter_debug_f32, in bytes: the n x n
+ * (padded 128 x 128) fp64 Gram, weights and flags of up to 8192 chunks at a
+ * time (longer layers are processed in batches of 8192 chunks). */
+int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes);
 
 /* mode 0: robust_estimator.filterL2 (src/robust_estimator.py:144-208);
  * mode 1: robust_estimator.ex_noregret (src/robust_estimator.py:42-133).
@@ -150,19 +166,22 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
  * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 128.
  * status: device int32, zeroed by the caller; set to 2 when an ex_noregret
  * projection has no feasible candidate (the reference then fails with
- * TypeError). */
+ * TypeError).  ex_noregret with ceil(eps*n) = 0 or fewer than 2 clients left
+ * after the Krum pre-filter -> SRA_ERR_ARG (the reference raises ValueError). */
 int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv, double eps,
-                   double sigma, double expansion, double* out, int32_t* status, void* stream);
+                   double sigma, double expansion, double* out, int32_t* status, void* ws, size_t ws_bytes,
+                   void* stream);
 
 /* Diagnostics variant: as sra_filter_f32, and additionally writes chunk 0's
  * centred Gram (128 x 128 fp64, row-major, zero-padded) followed by one record
  * of 144 doubles per filter iteration (weights before the update [128], top
- * eigenvalue, Lanczos steps, Ritz residual, restarts, 12 solver scalars) into dbg, which must hold
- * SRA_FILTER_DEBUG_DOUBLES doubles. */
+ * eigenvalue, Lanczos steps, Ritz residual, tridiagonal checks, active
+ * clients, w'Gw, restarts, second Gram-Schmidt passes, cycles) into dbg, which
+ * must hold SRA_FILTER_DEBUG_DOUBLES doubles. */
 #define SRA_FILTER_DEBUG_DOUBLES (128 * 128 + 256 * 144)
 int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
                          double eps, double sigma, double expansion, double* out, int32_t* status, double* dbg,
-                         void* stream);
+                         void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Cross-layer-norm clipping (k7): the stateful inline aggregators           */

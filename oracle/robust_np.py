@@ -161,6 +161,7 @@ def bulyan_median(arr):
     total |a_i - a_j| (numpy pairwise fp64 row sum, first index) and its row."""
     a = np.asarray(arr, dtype=np.float64)
     dist = np.abs(a[:, None] - a[None, :])
+    np.fill_diagonal(dist, 0.0)   # the reference never writes the diagonal (np.zeros): |inf - inf| is not NaN there
     total = dist.sum(axis=-1)
     m = int(np.argmin(total))
     return m, dist[m]
@@ -187,6 +188,8 @@ def bulyan_coordinates(selected, beta, block=2048):
     for lo in range(0, d, block):
         a = sel[lo:lo + block]
         cube = np.abs(a[:, :, None] - a[:, None, :])
+        idx = np.arange(a.shape[1])
+        cube[:, idx, idx] = 0.0   # diagonal stays 0 in the reference (np.zeros), even for inf / NaN values
         med = cube.sum(axis=-1).argmin(axis=-1)
         row = cube[np.arange(a.shape[0]), med]
         order = np.argsort(row, axis=-1)[:, :beta]
@@ -219,6 +222,13 @@ def _pw64(a):
     return _pw64(a[:n2]) + _pw64(a[n2:])
 
 
+def bulyan_keep(theta, beta):
+    """How many values ``arr[np.argsort(row)[:beta]]`` keeps (Python slice
+    semantics, robust_estimator.py:274): a negative beta (2f < N < 4f, e.g.
+    N=100 with malnum 30) drops -beta from the far end."""
+    return min(beta, theta) if beta >= 0 else max(theta + beta, 0)
+
+
 def bulyan_one_coordinate_leftfirst(arr, beta):
     """bulyan_one_coordinate with a DEFINED tie rule for the beta-nearest set.
 
@@ -227,28 +237,44 @@ def bulyan_one_coordinate_leftfirst(arr, beta):
     at exactly the same distance, which one enters the set depends on the numpy
     build (introsort in 1.21, x86-simd-sort AVX-512 in 2.x).  This restatement
     (and the GPU kernel) grows the window left-first on such ties; everywhere
-    else it equals the reference bit for bit."""
+    else it equals the reference bit for bit.  A NaN among the values makes
+    every total distance NaN, so np.argmin picks index 0 and NaN distances sort
+    last; infinities change the centre too (robust_estimator.py:261-275)."""
     a = np.asarray(arr, dtype=np.float64)
     theta = len(a)
+    keep = bulyan_keep(theta, beta)
+    if not np.isfinite(a).all():
+        # NaN makes every total NaN (argmin -> 0); one infinity makes every total
+        # infinite (-> 0); two equal infinities sit at NaN distance (-> the first
+        # of them).  Restated by definition: argsort of the distance row with NaN
+        # last, equal distances smaller value first, then index.
+        m, row = bulyan_median(a)
+        row = np.where(np.arange(theta) == m, 0.0, row)
+        key_nan = np.isnan(row)
+        order = np.lexsort((np.arange(theta), np.where(key_nan, 0.0, a), np.where(key_nan, 0.0, row), key_nan))
+        if keep == 0:
+            return np.nan
+        return _pw64([a[k] for k in order[:keep]]) / keep
     m, _ = bulyan_median(a)
     am = a[m]
     v = np.sort(a)
+    live = len(v)
+    if keep == 0:
+        return np.nan
     pl = int(np.searchsorted(v, am, side="left"))
     pr = int(np.searchsorted(v, am, side="right")) - 1
-    seq = [am] * min(pr - pl + 1, beta)
+    seq = [am] * min(pr - pl + 1, keep)
     l, r = pl, pr
-    while len(seq) < beta:
+    while len(seq) < keep:
         dl = am - v[l - 1] if l > 0 else np.inf
-        dr = v[r + 1] - am if r < theta - 1 else np.inf
+        dr = v[r + 1] - am if r < live - 1 else np.inf
         if dl <= dr:
             l -= 1
             seq.append(v[l])
         else:
             r += 1
             seq.append(v[r])
-    if beta <= 0:
-        return np.nan
-    return _pw64(seq) / beta
+    return _pw64(seq) / keep
 
 
 def bulyan_boundary_tie(arr, beta):
@@ -256,11 +282,12 @@ def bulyan_boundary_tie(arr, beta):
     both sides of the Bulyan median at exactly the boundary distance."""
     a = np.asarray(arr, dtype=np.float64)
     m, row = bulyan_median(a)
-    if beta <= 0 or beta >= len(a):
+    keep = bulyan_keep(len(a), beta)
+    if keep <= 0 or keep >= len(a) or np.isnan(a).any():
         return False
     dist = np.sort(row)
-    cut = dist[beta - 1]
-    if dist[beta] != cut:
+    cut = dist[keep - 1]
+    if dist[keep] != cut:
         return False
     at = a[row == cut]
     return bool((at < a[m]).any() and (at > a[m]).any())
@@ -401,6 +428,10 @@ def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7)
     keep = np.argpartition(scores, -f)[:-f]
     x = x[keep]
     m, k = x.shape
+    if m < 2:
+        # np.amax of the empty pairwise-distance list (f = 0 keeps nothing; one
+        # client has no pair) raises ValueError in the reference
+        raise ValueError("zero-size array to reduction operation maximum which has no identity")
     far = pairwise_l2(list(x))
     step = 0.5 / (np.amax(far[np.triu_indices(m, 1)]) ** 2)
     c = np.ones(m)

@@ -15,10 +15,17 @@
 //      middle order statistic; for even theta the lower and upper middles tie
 //      in exact arithmetic and numpy's fp64 pairwise row sum (8 accumulators,
 //      in selection order) decides -- emulated exactly here;
-//   3. the beta values nearest a_m (np.argsort of the distance row) form a
-//      contiguous window of the sorted values, grown left on <= ties;
+//   3. the `keep` values nearest a_m (np.argsort(row)[:beta] with Python slice
+//      semantics: keep = min(beta, theta) for beta >= 0, max(theta + beta, 0)
+//      for beta < 0, e.g. N=100, f=30 keeps 20) form a contiguous window of
+//      the sorted values, grown left on <= ties;
 //   4. their mean, summed in that (distance) order with numpy's pairwise
-//      scheme in fp64, is the output (float64, like the reference).
+//      scheme in fp64, is the output (float64, like the reference); keep = 0
+//      is the mean of an empty slice (NaN).
+//   A NaN among a coordinate's theta values makes every total distance NaN,
+//   so the reference's argmin picks index 0: the centre is then the first
+//   selected value, NaN distances sort last, and the result is NaN only when
+//   a NaN is among the kept values.
 #include "sra_common.hpp"
 
 namespace sra {
@@ -300,9 +307,63 @@ __global__ void __launch_bounds__(256) bulyan_pick_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 // per-coordinate Bulyan stage
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// The per-coordinate stage by definition, O(theta^2) per lane and no sort:
+//   T_i  = numpy pairwise fp64 sum of the distance row i (|a_i - a_k|, diagonal
+//          0 as np.zeros leaves it); m = np.argmin(T): the first NaN if any,
+//          else the first strict minimum;
+//   row  = distances[m]; argsort(row)[:beta] keeps `keep` values (slice
+//          semantics), NaN distances last, equal distances smaller value first
+//          (the left-first rule of the fast path), then index;
+//   res  = their numpy pairwise mean in that order.
+// Serves the drop-in's scalar helpers (any float64 input) and the columns of
+// the fused stage that hold a NaN or an infinity (NaN anywhere makes every T
+// NaN -> m = 0; one infinity makes every T infinite -> m = 0; two equal
+// infinities are at NaN distance -> m = the first of them).  `slot(p)` is
+// per-lane scratch for the rank -> value-index map.
+// ---------------------------------------------------------------------------
+template <typename A, typename Slot>
+__device__ double bulyan_stage_generic(A&& a, int theta, int keep, Slot&& slot, int* m_out) {
+  int m = 0;
+  double best = 0.0;
+  for (int i = 0; i < theta; ++i) {
+    const double ai = a(i);
+    const double T = np_pw64(0, theta, [&](int k) { return k == i ? 0.0 : __builtin_fabs(ai - a(k)); });
+    if (__builtin_isnan(T)) {
+      m = i;
+      break;
+    }
+    if (i == 0 || T < best) {
+      best = T;
+      m = i;
+    }
+  }
+  *m_out = m;
+  const double am = a(m);
+  auto dist = [&](int k) -> double { return k == m ? 0.0 : __builtin_fabs(am - a(k)); };
+  auto before = [&](int q, int k) -> bool {
+    const double dq = dist(q), dk = dist(k);
+    const bool nq = __builtin_isnan(dq), nk = __builtin_isnan(dk);
+    if (nq != nk) return nk;
+    if (!nq && dq != dk) return dq < dk;
+    if (!nq) {
+      const double vq = a(q), vk = a(k);
+      if (vq != vk) return vq < vk;
+    }
+    return q < k;
+  };
+  for (int k = 0; k < theta; ++k) {
+    int r = 0;
+    for (int q = 0; q < theta; ++q) r += (q != k && before(q, k)) ? 1 : 0;
+    slot(r) = k;
+  }
+  if (keep <= 0) return __builtin_nan("");
+  return np_pw64(0, keep, [&](int p) { return a(slot(p)); }) / static_cast<double>(keep);
+}
+
 template <int P>  // theta <= P; 64-thread blocks (one wave), sorted columns in LDS
 __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
-                                                          const int* __restrict__ rows, int theta, int beta,
+                                                          const int* __restrict__ rows, int theta, int keep,
                                                           int64_t d, double* __restrict__ out) {
   constexpr int P2 = next_pow2(P);
   __shared__ float col[P][64];
@@ -314,14 +375,14 @@ __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restric
   auto a_orig = [&](int i) -> float { return S[static_cast<int64_t>(rows[i]) * lds_ + j]; };
 
   float v[P2];
-  bool has_nan = false;
+  bool nonfinite = false;
 #pragma unroll
   for (int i = 0; i < P; ++i) {
     const float x = i < theta ? a_orig(i) : __builtin_inff();
-    has_nan |= __builtin_isnan(x);
+    nonfinite |= i < theta && !__builtin_isfinite(x);
     v[i] = x;
   }
-  if (__builtin_amdgcn_ballot_w64(has_nan) != 0) {
+  if (__builtin_amdgcn_ballot_w64(nonfinite) != 0) {
 #pragma unroll
     for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
   }
@@ -330,12 +391,23 @@ __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restric
   for (int i = 0; i < P; ++i) col[i][t] = v[i];
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
+  if (nonfinite) {
+    // a NaN or an infinity changes which value is the centre (see
+    // bulyan_stage_generic); this lane's own LDS column is its scratch
+    int m;
+    const double r = bulyan_stage_generic([&](int i) -> double { return a_orig(i); }, theta, keep,
+                                          [&](int p) -> int& { return *reinterpret_cast<int*>(&col[p][t]); }, &m);
+    if (t < rem) out[base + t] = r;
+    return;
+  }
+  const int live = theta;
 
-  // 1. Bulyan median: middle order statistic(s), fp64 pairwise tie-break
+  // 1. Bulyan median
   double am;
   if (theta & 1) {
     am = col[(theta - 1) / 2][t];
   } else {
+    // middle order statistics, fp64 pairwise tie-break
     const float L = col[theta / 2 - 1][t];
     const float U = col[theta / 2][t];
     if (L == U) {
@@ -358,54 +430,84 @@ __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restric
       }
     }
   }
-  // 2. run of values equal to a_m in the sorted column
-  int pl = (theta - 1) / 2, pr;
-  while (pl > 0 && static_cast<double>(col[pl][t]) > am) --pl;
-  while (pl < theta - 1 && static_cast<double>(col[pl][t]) < am) ++pl;
-  while (pl > 0 && static_cast<double>(col[pl - 1][t]) == am) --pl;
-  pr = pl;
-  while (pr + 1 < theta && static_cast<double>(col[pr + 1][t]) == am) ++pr;
-
-  // 3. beta nearest, in argsort (distance) order; 4. numpy pairwise fp64 mean
-  int l = pl, r = pr, taken = 0;
-  auto next = [&]() -> double {
-    // run elements first (distance 0), then grow left on <= ties
-    if (taken < pr - pl + 1) {
-      ++taken;
-      return am;
-    }
-    const double dl = l > 0 ? am - static_cast<double>(col[l - 1][t]) : __builtin_inf();
-    const double dr = r < theta - 1 ? static_cast<double>(col[r + 1][t]) - am : __builtin_inf();
-    ++taken;
-    if (dl <= dr) {
-      --l;
-      return static_cast<double>(col[l][t]);
-    }
-    ++r;
-    return static_cast<double>(col[r][t]);
-  };
   double res;
-  if (beta <= 0) {
-    res = __builtin_nan("");  // mean of an empty slice (beta = 0) / dropped tail
-  } else if (beta < 8) {
-    res = 0.0;
-    for (int i = 0; i < beta; ++i) res += next();
+  if (keep == 0) {
+    res = __builtin_nan("");   // mean of an empty slice
   } else {
-    // eight accumulators over the first beta - beta%8 values, then the tail
-    // (beta <= 128; a larger beta uses the same order with one accumulator
-    // set, within fp64 rounding of numpy's recursive split)
-    double r0 = next(), r1 = next(), r2 = next(), r3 = next(), r4 = next(), r5 = next(), r6 = next(), r7 = next();
-    int i = 8;
-    for (; i < beta - (beta % 8); i += 8) {
-      r0 += next(); r1 += next(); r2 += next(); r3 += next();
-      r4 += next(); r5 += next(); r6 += next(); r7 += next();
+    // 2. run of values equal to a_m in the sorted column (a_m is one of them)
+    int pl = (live - 1) / 2, pr;
+    while (pl > 0 && static_cast<double>(col[pl][t]) > am) --pl;
+    while (pl < live - 1 && static_cast<double>(col[pl][t]) < am) ++pl;
+    while (pl > 0 && static_cast<double>(col[pl - 1][t]) == am) --pl;
+    pr = pl;
+    while (pr + 1 < live && static_cast<double>(col[pr + 1][t]) == am) ++pr;
+
+    // 3. the keep nearest, in argsort (distance) order; 4. numpy pairwise fp64 mean
+    int l = pl, r = pr, taken = 0;
+    auto next = [&]() -> double {
+      // run elements first (distance 0), then grow left on <= ties
+      if (taken < pr - pl + 1) {
+        ++taken;
+        return am;
+      }
+      const double dl = l > 0 ? am - static_cast<double>(col[l - 1][t]) : __builtin_inf();
+      const double dr = r < live - 1 ? static_cast<double>(col[r + 1][t]) - am : __builtin_inf();
+      ++taken;
+      if (dl <= dr) {
+        --l;
+        return static_cast<double>(col[l][t]);
+      }
+      ++r;
+      return static_cast<double>(col[r][t]);
+    };
+    if (keep < 8) {
+      res = 0.0;
+      for (int i = 0; i < keep; ++i) res += next();
+    } else {
+      // eight accumulators over the first keep - keep%8 values, then the tail
+      // (keep <= theta <= 128)
+      double r0 = next(), r1 = next(), r2 = next(), r3 = next(), r4 = next(), r5 = next(), r6 = next(), r7 = next();
+      int i = 8;
+      for (; i < keep - (keep % 8); i += 8) {
+        r0 += next(); r1 += next(); r2 += next(); r3 += next();
+        r4 += next(); r5 += next(); r6 += next(); r7 += next();
+      }
+      res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+      for (; i < keep; ++i) res += next();
     }
-    res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < beta; ++i) res += next();
+    res = res / static_cast<double>(keep);
   }
-  res = res / static_cast<double>(beta);
-  if (has_nan) res = __builtin_nan("");
   if (t < rem) out[base + t] = res;
+}
+
+// arr[np.argsort(distances)[:beta]] keeps min(beta, theta) values for beta >= 0
+// and max(theta + beta, 0) for beta < 0 (Python slice semantics,
+// robust_estimator.py:274; torch slicing at src/DBA/helper.py:939 likewise)
+inline int bulyan_keep(int theta, int beta) {
+  if (beta >= 0) return beta < theta ? beta : theta;
+  return theta + beta > 0 ? theta + beta : 0;
+}
+
+// the drop-in's scalar helpers: one lane per column of a float64 theta x d matrix
+constexpr int kCoordMaxTheta = 512;
+
+__global__ void __launch_bounds__(64) bulyan_coord_f64_kernel(const double* __restrict__ A, int theta, int64_t d,
+                                                              int64_t lda, int keep, double* __restrict__ out,
+                                                              int64_t* __restrict__ midx, double* __restrict__ mrow,
+                                                              int64_t ldr) {
+  __shared__ int order[kCoordMaxTheta][64];
+  const int t = threadIdx.x;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + t;
+  if (j >= d) return;
+  auto a = [&](int i) -> double { return A[static_cast<int64_t>(i) * lda + j]; };
+  int m;
+  out[j] = bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return order[p][t]; }, &m);
+  if (midx) midx[j] = m;
+  if (mrow) {
+    const double am = a(m);
+    for (int k = 0; k < theta; ++k)
+      mrow[static_cast<int64_t>(k) * ldr + j] = k == m ? 0.0 : __builtin_fabs(am - a(k));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -455,11 +557,12 @@ static int launch_select_rows(const float* X, int64_t ldx, const int* rows, int 
 
 static int launch_final(const float* S, int64_t lds_, const int* rows, int theta, int beta, int64_t d, double* out,
                         hipStream_t s) {
+  const int keep = bulyan_keep(theta, beta);
   const int64_t blocks = cdiv(d, 64);
   const int P = static_cast<int>(cdiv(theta, 16) * 16);
 #define SRA_FIN(PP)                                                                                              \
   case PP:                                                                                                       \
-    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(blocks), dim3(64), 0, s, S, lds_, rows, theta, beta, d, out); \
+    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(blocks), dim3(64), 0, s, S, lds_, rows, theta, keep, d, out); \
     return launch_status("bulyan_final_kernel");
   switch (P) {
     SRA_FIN(16) SRA_FIN(32) SRA_FIN(48) SRA_FIN(64) SRA_FIN(80) SRA_FIN(96) SRA_FIN(112) SRA_FIN(128)
@@ -571,4 +674,17 @@ extern "C" int sra_bulyan_dba_f32(const float* X, int64_t n, int64_t d, int64_t 
               "DBA bulyan_krum with f = 1 (its last round scores an empty neighbour set) is not supported");
   return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
                        static_cast<hipStream_t>(stream), true);
+}
+
+extern "C" int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t d, int64_t lda, int32_t beta,
+                                         double* out, int64_t* median_index, double* median_row, int64_t ldr,
+                                         void* stream) {
+  SRA_REQUIRE(A != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(theta >= 1 && theta <= kCoordMaxTheta, SRA_ERR_UNSUPPORTED, "1 <= theta <= %d (got %lld)",
+              kCoordMaxTheta, static_cast<long long>(theta));
+  SRA_REQUIRE(d >= 1 && lda >= d && (median_row == nullptr || ldr >= d), SRA_ERR_SHAPE, "bad d / lda / ldr");
+  const int keep = bulyan_keep(static_cast<int>(theta), beta);
+  hipLaunchKernelGGL(bulyan_coord_f64_kernel, dim3(cdiv(d, 64)), dim3(64), 0, static_cast<hipStream_t>(stream), A,
+                     static_cast<int>(theta), d, lda, keep, out, median_index, median_row, ldr);
+  return launch_status("bulyan_coord_f64_kernel");
 }

@@ -4,35 +4,43 @@
 // Replaces src/robust_estimator.py:42-133 (ex_noregret_, ex_noregret) and
 // :144-208 (filterL2_, filterL2).  Each layer is cut into itv-wide chunks
 // (restarting at every layer, last chunk partial); each chunk is filtered
-// independently.  One 256-thread workgroup per chunk (persistent over chunks).
+// independently.  The reference forms the k x k (k <= itv = 1000) fp64
+// weighted covariance from N outer products and calls eigh for its top
+// eigenpair, 2*int(eps*N) times per chunk.  Here everything after one pass
+// over the chunk runs in client space (n x n, n <= 128), in four launches per
+// batch of chunks (the n x n Gram of every chunk of the batch lives in the
+// caller's workspace between them):
 //
-// The reference builds the k x k (k <= itv = 1000) fp64 weighted covariance
-// from N outer products and calls eigh for its top eigenpair, 2*int(eps*N)
-// times per chunk.  Here everything after one pass over the chunk runs in
-// client space (n x n, n <= 128):
-//
-//   Phase A  centred chunk Gram G = Z Z^T, Z = X_chunk - column mean, on the
-//            fp64 MFMA (v_mfma_f64_16x16x4_f64), 36 upper 16x16 tiles over 4
-//            waves; G then lives in registers (two lanes per row, 64 fp64 each).
-//   Phase C  per iteration, with weights w = c / sum(c):
-//              C = G - g 1^T - 1 g^T + s 1 1^T  (g = G w, s = w^T G w) is the
-//              Gram of x_i - mu (mu the weighted mean), so the covariance's
-//              nonzero spectrum is that of M = W^1/2 C W^1/2;
-//              top eigenpair (lambda, u) of M by Lanczos with full
-//              reorthogonalisation (fp64) + multisection bisection on the
-//              tridiagonal + inverse iteration;
-//              tau_j = ((x_j - mu).v)^2 = (C W^1/2 u)_j^2 / lambda;
-//              early exit if lambda^2 <= expansion * sigma^2;
-//              filterL2: c *= 1 - tau/tau_max, drop argmax, c /= |c|_1;
-//              ex_noregret: c *= 1 - step*tau, KL projection onto the capped
-//              simplex (every candidate evaluated in parallel, numpy's
-//              pairwise fp64 sums emulated for the feasibility tests and KL).
-//            ex_noregret first drops the ceil(eps*n) clients with the largest
-//            Krum scores (fp32 distances from G, numpy pairwise score sums)
-//            and sets step = 0.5 / max pairwise distance^2 in fp32.
-//   Phase D  mu_j = sum_i c_i x_ij / sum_i c_i in fp64 over the kept clients
-//            in client order (the reference's np.average), second pass over
-//            the chunk (L2-resident).
+//   chunk_gram_kernel   centred chunk Gram G = Z Z^T, Z = X_chunk - column
+//                       mean, on the fp64 MFMA (v_mfma_f64_16x16x4_f64), one
+//                       256-thread workgroup per chunk; HBM / MFMA bound.
+//   noregret_pre_kernel ex_noregret only: Krum pre-filter of the chunk (fp32
+//                       distances from G, numpy pairwise score sums, the
+//                       ceil(eps*n) largest scores dropped) and the step size
+//                       0.5 / max pairwise distance^2 in fp32.
+//   filter_solve_kernel the iterations, one 256-thread workgroup per chunk
+//                       (two per CU), G resident in registers (a row per lane
+//                       pair).  Per iteration, with w = c / sum(c):
+//                         C = G - g 1^T - 1 g^T + s 1 1^T (g = G w, s = w^T G w)
+//                         is the Gram of x_i - mu, so the covariance's nonzero
+//                         spectrum is that of M = W^1/2 C W^1/2;
+//                         top eigenpair (lambda, u) of M by Lanczos with full
+//                         re-orthogonalisation (classical Gram-Schmidt, a second
+//                         pass only under heavy cancellation) and deferred
+//                         normalisation: three barriers per step; the
+//                         tridiagonal's top eigenpair (multisection on Sturm
+//                         counts, eigenvector from the bottom pivots) only at
+//                         predicted convergence points, computed redundantly by
+//                         every wave (no extra barrier);
+//                         tau_j = ((x_j - mu).v)^2 = (C W^1/2 u)_j^2 / lambda;
+//                         early exit if lambda^2 <= expansion * sigma^2;
+//                         filterL2: c *= 1 - tau/tau_max, drop argmax, c /= |c|_1;
+//                         ex_noregret: c *= 1 - step*tau, KL projection onto the
+//                         capped simplex (every candidate evaluated in parallel,
+//                         numpy's pairwise fp64 sums emulated).
+//   chunk_mean_kernel   mu_j = sum_i c_i x_ij / sum_i c_i in fp64 over the kept
+//                       clients in client order (the reference's np.average),
+//                       one lane per coordinate; HBM bound.
 #include "sra_common.hpp"
 
 namespace sra {
@@ -40,38 +48,24 @@ namespace sra {
 constexpr int FNP = 128;           // padded client count
 constexpr int FST = 64;            // coordinates per Gram stage
 constexpr int FROW = FST + 4;      // stage row stride (floats)
-constexpr int LMAX = 62;           // Lanczos steps per restart (V fills the 64 KB union)
-constexpr int VST = FNP + 4;       // Lanczos basis row stride (doubles): spreads rows over LDS banks
-constexpr int LRESTART = 6;        // explicit restarts from the Ritz vector
+constexpr int LMAX = 59;           // Lanczos basis capacity (LDS)
+constexpr int VST = 136;           // basis row stride (doubles): the 4 rows one ds_read_b128 lane group
+                                   // touches start 16 banks apart
+constexpr int XOFF = 66;           // vector buffers: entries [64, 128) start at XOFF (bank-disjoint halves)
+constexpr int XLEN = XOFF + 64 + 2;
+constexpr int TRI = 256;           // per-wave tridiagonal record: alpha[64] beta^2[64] s / dp[64] dm[64]
+constexpr double kResTol = 1e-13;  // converged when the Ritz residual <= kResTol * lambda
+constexpr double kDgks = 0.5;      // second Gram-Schmidt pass when |r|^2 < kDgks * |r'|^2 (DGKS)
+constexpr int kMaxRestarts = 8;
+constexpr int kBatch = 8192;       // chunks per workspace batch
+constexpr int kMisc = 8;           // per-chunk scalars: [0] np.average scale, [1] ex_noregret step
 
-struct FilterShared {
-  // union region: stage buffer (Phase A) / G transfer half (Phase B) /
-  // Lanczos basis V[k][i] (Phase C) / Krum distance rows (ex_noregret)
-  static constexpr int kUnionBytes = 65536;
-  static constexpr int kVec = FNP;  // doubles per vector
-};
+// per-iteration diagnostics of chunk 0 (sra_filter_debug_f32): FNP weights
+// before the update, then lambda, Lanczos steps, Ritz residual, checks, active
+// clients, w'Gw, restarts, second Gram-Schmidt passes, cycles of the iteration
+constexpr int kDbgRec = FNP + 16;
 
-struct FilterArgs {
-  const float* X;
-  int n;
-  int64_t d;
-  int64_t ldx;
-  int itv;
-  int nchunks;
-  double eps;
-  double sigma;
-  double expansion;
-  double* out;
-  int* status;
-  double* dbg;   // optional diagnostics of chunk 0 (see sra_filter_debug_f32)
-};
-
-// diagnostics layout (doubles): [0, FNP*FNP) chunk-0 Gram; then per outer
-// iteration it a record of FNP+4: c[0..FNP) before the update, lam, Lanczos
-// steps, Ritz residual, restarts used, then 12 solver scalars (scal[4..15]).
-constexpr int kDbgRec = 128 + 16;
-
-// ----- wave / block helpers (256 threads) --------------------------------------
+// ----- wave helpers ---------------------------------------------------------
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
   const long long b = __builtin_bit_cast(long long, v);
@@ -84,10 +78,6 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), l);
   const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), l);
   return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
-}
-// v with lane l replaced by x (l uniform)
-__device__ __forceinline__ double writelane_f64(double x, int l, double v) {
-  return static_cast<int>(threadIdx.x & 63) == l ? x : v;
 }
 // sum over the wave, identical in every lane (DPP within rows, readlane across)
 __device__ __forceinline__ double wave_sum(double v) {
@@ -105,17 +95,17 @@ __device__ __forceinline__ double wave_max(double v) {
   return fmax(fmax(readlane_f64(v, 0), readlane_f64(v, 16)), fmax(readlane_f64(v, 32), readlane_f64(v, 48)));
 }
 __device__ __forceinline__ double wave_min(double v) { return -wave_max(-v); }
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  const double r = (red[0] + red[1]) + (red[2] + red[3]);
-  __syncthreads();
-  return r;
+
+// a / b from the hardware reciprocal with one Newton step and one residual
+// correction (within an ulp or two; pivots of the tridiagonal only)
+__device__ __forceinline__ double fdiv(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);
 }
 
-// numpy pairwise fp32 sum of f(0..n) (n <= 255 via one or two splits)
+// numpy pairwise fp32 sum of f(0..n) (n <= 255 via one split)
 template <typename F>
 __device__ float np_pw32(int n, F&& f) {
   auto block = [&](int lo, int m) -> float {
@@ -141,11 +131,20 @@ __device__ float np_pw32(int n, F&& f) {
   return block(0, n2) + block(n2, n - n2);
 }
 
-// 36 upper-triangle 16x16 tiles (I <= J) of the 128 x 128 chunk Gram
-__constant__ int kFTileI[36] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2,
-                                2, 2, 2, 3, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 6, 6, 7};
-__constant__ int kFTileJ[36] = {0, 1, 2, 3, 4, 5, 6, 7, 1, 2, 3, 4, 5, 6, 7, 2, 3, 4,
-                                5, 6, 7, 3, 4, 5, 6, 7, 4, 5, 6, 7, 5, 6, 7, 6, 7, 7};
+// ============================================================================
+// chunk_gram_kernel
+// ============================================================================
+struct GramArgs {
+  const float* X;
+  int n;
+  int64_t d;
+  int64_t ldx;
+  int itv;
+  int64_t chunk0;   // first chunk of the batch
+  int nb;           // chunks in the batch
+  double* G;        // [nb][FNP][FNP]
+};
+
 constexpr int ftile_i(int t) {
   int c = 0;
   for (int i = 0; i < 8; ++i)
@@ -165,19 +164,17 @@ constexpr int ftile_j(int t) {
   return 0;
 }
 
-// Phase A for wave W: its 9 tiles (W + 4t) accumulate G over the chunk in
-// 64-coordinate stages staged through LDS and centred by the stage's column
-// means (fp64); tile -> row block mapping is compile-time.
+// wave W's 9 upper tiles (W + 4t) of the 36 16x16 tiles accumulate G over the
+// chunk in 64-coordinate stages staged through LDS and centred by the stage's
+// column means (fp64); the tile -> row block mapping is compile-time.
 template <int W>
-__device__ __forceinline__ void filter_gram_phase(const FilterArgs& A, int64_t k0, int k, char* uni,
-                                                  f64x4 (&acc)[9]) {
+__device__ __forceinline__ void gram_tiles(const GramArgs& A, int64_t k0, int k, float* stage, double* smean,
+                                           f64x4 (&acc)[9]) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int n = A.n;
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-  float* stage = reinterpret_cast<float*>(uni);
-  double* smean = reinterpret_cast<double*>(uni + FNP * FROW * 4);
   for (int s0 = 0; s0 < k; s0 += FST) {
     for (int e = tid; e < FNP * FST; e += 256) {
       const int r = e / FST, cc = e - (e / FST) * FST;
@@ -186,10 +183,14 @@ __device__ __forceinline__ void filter_gram_phase(const FilterArgs& A, int64_t k
       stage[r * FROW + cc] = v;
     }
     __syncthreads();
-    if (tid < FST) {
+    {
+      // column means: 4 lanes per column, interleaved rows, quad reduction
+      const int cc = tid >> 2, part = tid & 3;
       double sm = 0.0;
-      for (int r = 0; r < n; ++r) sm += static_cast<double>(stage[r * FROW + tid]);
-      smean[tid] = sm / n;
+      for (int r = part; r < n; r += 4) sm += static_cast<double>(stage[r * FROW + cc]);
+      sm += dpp_f64<0xB1>(sm);
+      sm += dpp_f64<0x4E>(sm);
+      if (part == 0) smean[cc] = sm / n;
     }
     __syncthreads();
 #pragma unroll 2
@@ -203,792 +204,881 @@ __device__ __forceinline__ void filter_gram_phase(const FilterArgs& A, int64_t k
         fr[b] = r < n ? static_cast<double>(stage[r * FROW + cc]) - mu : 0.0;
       }
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      for (int t = 0; t < 9; ++t)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[ftile_i(W + 4 * t)], fr[ftile_j(W + 4 * t)], acc[t], 0, 0, 0);
-      }
     }
     __syncthreads();
   }
 }
 
-// ----- block reductions (256 threads = 4 waves) -------------------------------
-__device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red[wave] = a;
-    red[4 + wave] = b;
+template <int W>
+__device__ __forceinline__ void gram_store(double* G, const f64x4 (&acc)[9]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int I = ftile_i(W + 4 * t), J = ftile_j(W + 4 * t);
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      // f64 16x16x4 C/D layout: col = lane & 15, row = (lane >> 4) + 4 * reg
+      const int row = 16 * I + (lane >> 4) + 4 * rg;
+      const int col = 16 * J + (lane & 15);
+      G[row * FNP + col] = acc[t][rg];
+      if (I != J) G[col * FNP + row] = acc[t][rg];
+    }
   }
-  __syncthreads();
-  a = (red[0] + red[1]) + (red[2] + red[3]);
-  b = (red[4] + red[5]) + (red[6] + red[7]);
-  __syncthreads();
 }
 
-// index of the largest v (first index on ties); inactive lanes pass -inf.
-// Returns the index; *vbest receives its value.
-__device__ __forceinline__ int block_argmax_first(double v, int i, double* red, int* ired, double* vbest) {
+__global__ void __launch_bounds__(256) chunk_gram_kernel(GramArgs A) {
+  __shared__ __attribute__((aligned(16))) float stage[FNP * FROW];
+  __shared__ double smean[FST];
+  const int b = blockIdx.x;
+  const int64_t k0 = (A.chunk0 + b) * static_cast<int64_t>(A.itv);
+  const int k = static_cast<int>((k0 + A.itv < A.d ? k0 + A.itv : A.d) - k0);
+  double* G = A.G + static_cast<size_t>(b) * FNP * FNP;
+  f64x4 acc[9];
+  switch (threadIdx.x >> 6) {
+    case 0: gram_tiles<0>(A, k0, k, stage, smean, acc); gram_store<0>(G, acc); break;
+    case 1: gram_tiles<1>(A, k0, k, stage, smean, acc); gram_store<1>(G, acc); break;
+    case 2: gram_tiles<2>(A, k0, k, stage, smean, acc); gram_store<2>(G, acc); break;
+    default: gram_tiles<3>(A, k0, k, stage, smean, acc); gram_store<3>(G, acc); break;
+  }
+}
+
+// ============================================================================
+// noregret_pre_kernel: ex_noregret's Krum pre-filter (robust_estimator.py:47-58)
+// ============================================================================
+struct PreArgs {
+  const double* G;
+  int* act;        // [nb][FNP] out: kept clients
+  double* misc;    // [nb][kMisc] out: [1] step
+  int n;
+  int nb;
+  double eps;
+};
+
+__global__ void __launch_bounds__(256) noregret_pre_kernel(PreArgs A) {
+  __shared__ float drow[FNP * FNP];   // fp32 distances, rows sorted in place
+  __shared__ double diag[FNP];
+  __shared__ double score[FNP];
+  __shared__ int keep[FNP];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = A.n;
+  const int b = blockIdx.x;
+  const double* G = A.G + static_cast<size_t>(b) * FNP * FNP;
+  const int fp = static_cast<int>(ceil(A.eps * n));
+  if (tid < FNP) diag[tid] = G[tid * FNP + tid];
+  __syncthreads();
+  // krum_'s np.linalg.norm in fp32: sqrt of the centred-Gram squared distance
+  for (int e = tid; e < FNP * FNP; e += 256) {
+    const int i = e >> 7, j = e & (FNP - 1);
+    if (i < n && j < n) {
+      const double sq = diag[i] + diag[j] - 2.0 * G[e];
+      drow[e] = i == j ? 0.f : static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
+    }
+  }
+  __syncthreads();
+  // one wave per row: its n-1 off-diagonal distances (+inf padded to 128)
+  // sorted by a register bitonic network, 2 elements per lane
+  for (int row = wave; row < n; row += 4) {
+    auto ld = [&](int e) -> float {
+      if (e >= n - 1) return __builtin_inff();
+      return drow[row * FNP + (e < row ? e : e + 1)];
+    };
+    float v0 = ld(2 * lane), v1 = ld(2 * lane + 1);
+#pragma unroll
+    for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride >= 1; stride >>= 1) {
+        const bool asc = ((2 * lane) & size) == 0;
+        if (stride == 1) {
+          const float lo = fminf(v0, v1), hi = fmaxf(v0, v1);
+          v0 = asc ? lo : hi;
+          v1 = asc ? hi : lo;
+        } else {
+          const int ls = stride >> 1;
+          const float p0 = __shfl_xor(v0, ls), p1 = __shfl_xor(v1, ls);
+          const bool takemin = asc != ((lane & ls) != 0);
+          v0 = takemin ? fminf(v0, p0) : fmaxf(v0, p0);
+          v1 = takemin ? fminf(v1, p1) : fmaxf(v1, p1);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    drow[row * FNP + 2 * lane] = v0;
+    drow[row * FNP + 2 * lane + 1] = v1;
+  }
+  __syncthreads();
+  // score = numpy pairwise fp32 sum of the m smallest (Python slice semantics)
+  const int m = n - fp - 2 >= 0 ? (n - fp - 2 < n - 1 ? n - fp - 2 : n - 1)
+                                : ((n - 1) + (n - fp - 2) > 0 ? (n - 1) + (n - fp - 2) : 0);
+  if (tid < n) {
+    const float* rw = drow + tid * FNP;
+    score[tid] = static_cast<double>(np_pw32(m, [&](int q) { return rw[q]; }));
+  }
+  __syncthreads();
+  // argpartition(metric, -f)[:-f]: drop the fp largest scores (ties: the later
+  // index is dropped first; numpy's introselect order on exact ties is not
+  // pinned by any fixture)
+  if (tid < FNP) {
+    int kp = 0;
+    if (tid < n) {
+      const double si = score[tid];
+      int above = 0;
+      for (int j = 0; j < n; ++j) above += (score[j] > si || (score[j] == si && j > tid)) ? 1 : 0;
+      kp = above >= fp ? 1 : 0;
+    }
+    keep[tid] = kp;
+    A.act[static_cast<size_t>(b) * FNP + tid] = kp;
+  }
+  __syncthreads();
+  // step = 0.5 / max pairwise fp32 distance^2 among the kept clients (fp32
+  // arithmetic: numpy 2 keeps the float32 scalar)
+  float md = 0.f;
+  for (int e = tid; e < FNP * FNP; e += 256) {
+    const int i = e >> 7, j = e & (FNP - 1);
+    if (i < n && j < n && i < j && keep[i] && keep[j]) {
+      const double sq = diag[i] + diag[j] - 2.0 * G[e];
+      const float dd = static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
+      md = dd > md ? dd : md;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float o = __shfl_xor(md, off);
+    md = o > md ? o : md;
+  }
+  if (lane == 0) red[wave] = md;
+  __syncthreads();
+  if (tid == 0) {
+    float mx = red[0];
+    for (int q = 1; q < 4; ++q) mx = red[q] > mx ? red[q] : mx;
+    A.misc[static_cast<size_t>(b) * kMisc + 1] = static_cast<double>(0.5f / (mx * mx));
+  }
+}
+
+// ============================================================================
+// filter_solve_kernel
+// ============================================================================
+struct SolveArgs {
+  const double* G;   // [nb][FNP][FNP]
+  double* c;         // [nb][FNP] out: final weights
+  int* act;          // [nb][FNP] in (ex_noregret: the pre-filter's kept set) / out: kept
+  double* misc;      // [nb][kMisc]
+  int* status;
+  int n;
+  int nb;
+  double eps;
+  double sigma;
+  double expansion;
+  double* dbg;       // optional diagnostics of the batch's chunk 0
+};
+
+constexpr size_t kSolveLds =
+    sizeof(double) * (static_cast<size_t>(LMAX) * VST + 2 * XLEN + 64 + 32 + 4 * TRI + 4 * FNP) +
+    sizeof(int) * (3 * FNP + 16);
+static_assert(2 * kSolveLds <= 163840, "two solver workgroups must fit one CU's LDS");
+
+// Top eigenpair of the Lanczos tridiagonal T_m (alpha in trw[0, m), beta^2 in
+// trw[64, 64 + m - 1)), evaluated identically by every wave of the block:
+// multisection on Sturm counts (the division-free recurrence of the leading
+// principal minors, rescaled every 4 steps; the previous check's Ritz value
+// theta_lb is a lower bound by interlacing, so the first round's points are
+// geometric above it), then the eigenvector from a twisted factorisation of
+// T - lambda I (lane 0 runs the forward pivots, lane 1 the backward ones, the
+// twist is the smallest |gamma|).  The normalised eigenvector goes to
+// trw[128, 128 + m); returns lambda and its last component.  Kept out of line:
+// it runs a few times per filter iteration and its registers would otherwise
+// compete with the 64 Gram values per lane of the solver's hot loop.
+__device__ __attribute__((noinline)) void tri_top(double* trw, int m, double tscale, double theta_lb, double* lam_out,
+                                                  double* zlast_out) {
+  const int lane = threadIdx.x & 63;
+  const double al = lane < m ? trw[lane] : 0.0;
+  const double b2l = lane + 1 < m ? trw[64 + lane] : 0.0;
+  const double bl = lane + 1 < m ? sqrt(trw[64 + lane]) : 0.0;
+  const double bp = (lane >= 1 && lane < m) ? sqrt(trw[64 + lane - 1]) : 0.0;
+  const double rad = fabs(bp) + fabs(bl);
+  double lo = wave_min(lane < m ? al - rad : 1e300);
+  double hi = wave_max(lane < m ? al + rad : -1e300);
+  // multisection on Sturm counts: the division-free recurrence of the
+  // leading principal minors, rescaled by powers of two every 4
+  // steps; the previous check's Ritz value is a lower bound
+  // (interlacing), so the first round's points are geometric above it
+  const bool geo = theta_lb > lo && theta_lb < hi;
+  if (geo) lo = theta_lb;
+  for (int round = 0; round < 16; ++round) {
+    const double fr = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, lane - 63) : (lane + 1) / 65.0;
+    const double x = lo + (hi - lo) * fr;
+    double p2 = 1.0;
+    double p1 = readlane_f64(al, 0) - x;
+    int cntb = __builtin_signbit(p1) ? 1 : 0;
+#pragma unroll 4
+    for (int q = 1; q < m; ++q) {
+      // alpha / beta^2 broadcast from registers (readlane), off the FMA chain
+      const double pk = fma(readlane_f64(al, q) - x, p1, -(readlane_f64(b2l, q - 1) * p2));
+      cntb += (__builtin_signbit(pk) ? 1 : 0) != (__builtin_signbit(p1) ? 1 : 0);
+      p2 = p1;
+      p1 = pk;
+      if ((q & 3) == 3) {
+        const int e = __builtin_amdgcn_frexp_exp(p1);
+        p1 = __builtin_amdgcn_ldexp(p1, -e);
+        p2 = __builtin_amdgcn_ldexp(p2, -e);
+      }
+    }
+    const unsigned long long ok = __builtin_amdgcn_ballot_w64(cntb >= m);
+    const int first = ok ? __builtin_ctzll(ok) : 64;
+    const double flo = first == 0 ? 0.0
+                                  : ((geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 64)
+                                                         : first / 65.0);
+    const double fhi = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 63) : (first + 1) / 65.0;
+    const double nlo = lo + (hi - lo) * flo;
+    const double nhi = first < 64 ? lo + (hi - lo) * fhi : hi;
+    lo = nlo;
+    hi = nhi;
+    if (hi - lo <= 2e-16 * fmax(fabs(lo), fabs(hi))) break;
+  }
+  const double lm = 0.5 * (lo + hi);
+  // eigenvector of T - lm I by a twisted factorisation: lane 0 runs the
+  // forward pivots dp (into s), lane 1 the backward pivots dm (into the
+  // scratch) in one serial loop; the twist is the smallest |gamma|
+  const double tiny = 1e-300 + 1e-30 * tscale;
+  if (lane < 2) {
+    const bool fw = lane == 0;
+    double piv = 0.0;
+    for (int k = 0; k < m; ++k) {
+      const int q = fw ? k : m - 1 - k;
+      double v = trw[q] - lm;
+      if (k > 0) v -= fdiv(trw[64 + (fw ? q - 1 : q)], piv);
+      if (fabs(v) < tiny) v = -tiny;
+      piv = v;
+      trw[(fw ? 128 : 192) + q] = v;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const double dpl = lane < m ? trw[128 + lane] : 0.0;
+  const double dml = lane < m ? trw[192 + lane] : 0.0;
+  const double dmn = lane + 1 < m ? trw[192 + lane + 1] : 1.0;
+  double gam = lane < m ? fabs(dpl + dml - (al - lm)) : 1e308;
+  int tw = lane;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double og = __shfl_xor(gam, off);
+    const int ot = __shfl_xor(tw, off);
+    if (og < gam || (og == gam && ot < tw)) {
+      gam = og;
+      tw = ot;
+    }
+  }
+  tw = __builtin_amdgcn_readfirstlane(tw);
+  // z_tw = 1; z_q = -(b_q / dp_q) z_{q+1} below the twist,
+  // z_{q+1} = -(b_q / dm_{q+1}) z_q above it: ratios per lane, then
+  // lane 0 walks down and lane 1 up (into s)
+  const double rat = lane < tw ? -bl / dpl : (lane + 1 < m ? -bl / dmn : 0.0);
+  __builtin_amdgcn_wave_barrier();
+  if (lane < m) trw[192 + lane] = rat;
+  __builtin_amdgcn_wave_barrier();
+  if (lane < 2) {
+    const bool down = lane == 0;
+    double z = 1.0;
+    if (down) trw[128 + tw] = 1.0;
+    const int steps = down ? tw : m - 1 - tw;
+    for (int k = 0; k < steps; ++k) {
+      const int q = down ? tw - 1 - k : tw + k;   // ratio index
+      z *= trw[192 + q];
+      if (fabs(z) > 1e150) z = copysign(1e150, z);   // z_tw = 1 is the largest in exact arithmetic
+      trw[128 + (down ? q : q + 1)] = z;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  double zv = lane < m ? trw[128 + lane] : 0.0;
+  const double amax = wave_max(fabs(zv));
+  const double zs = zv / amax;
+  zv = zs / sqrt(wave_sum(zs * zs));
+  if (lane < m) trw[128 + lane] = zv;
+  *lam_out = lm;
+  *zlast_out = readlane_f64(zv, m - 1);
+}
+
+// ex_noregret's projection (robust_estimator.py:77-99) onto {sum c = 1,
+// c <= cap} over the nk kept clients: candidate i caps the i+1 largest weights
+// and rescales the rest; the feasible candidate with the smallest
+// KL(c || c_) = sum_{q<=i} c_q log(c_q / cap) - log(scale) * sum_{q>i} c_q wins
+// (first on ties); the reference's loop stops at the first infeasible clip.
+// Once per filter iteration, so it is kept out of line: the solver's 64 Gram
+// registers per lane stay put while this runs.  Returns false when no
+// candidate is feasible.  Block-wide (all 256 lanes), barriers inside.
+__device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int row, bool own, int nk, double cap,
+                                                     double* cvec, double* vscr, int* ibuf, double* red,
+                                                     double* hbuf) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int* kidx = ibuf;            // compact -> client row
+  int* irank = ibuf + FNP;     // descending rank of a compact entry
+  int* flag = ibuf + 2 * FNP;  // active flags
+  int* islot = ibuf + 3 * FNP; // argmax indices
+  double* cc = vscr;           // compact weights
+  double* sv = vscr + FNP;     // weights in descending order
+  double* hl = vscr + 2 * FNP; // sv * log(sv / cap)
+  const double ci = *ci_io;
+  if (own) flag[row] = ai ? 1 : 0;
+  __syncthreads();
+  if (own && ai) {
+    int pos = 0;
+    for (int q2 = 0; q2 < row; ++q2) pos += flag[q2];
+    kidx[pos] = row;
+    cc[pos] = ci;
+  }
+  __syncthreads();
+  // descending rank; ties: later compact index first (flip of a stable ascending argsort)
+  if (tid < nk) {
+    const double v = cc[tid];
+    int rk = 0;
+    for (int q2 = 0; q2 < nk; ++q2) rk += (cc[q2] > v || (cc[q2] == v && q2 > tid)) ? 1 : 0;
+    irank[tid] = rk;
+    sv[rk] = v;
+    hl[rk] = v * log(v / cap);
+  }
+  __syncthreads();
+  double negkl = -__builtin_inf(), scale = 0.0;
+  int stop = 1 << 30;
+  if (tid < nk) {
+    const int i = tid;
+    const double clip = 1.0 - np_pw64(0, i + 1, [&](int) { return cap; });
+    if (clip <= 0.0) {
+      stop = i;
+    } else if (i + 1 < nk) {
+      const double norm = np_pw64(i + 1, nk - i - 1, [&](int q2) { return sv[q2]; });
+      scale = clip / norm;
+      if (!(sv[i + 1] * scale > cap)) {
+        double head = 0.0;
+        for (int q2 = 0; q2 <= i; ++q2) head += hl[q2];
+        negkl = -(head - norm * log(scale));
+      }
+    }
+  }
+  // first infeasible clip (block min of stop), then the first best candidate before it
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int o2 = __shfl_xor(stop, off);
+    stop = o2 < stop ? o2 : stop;
+  }
+  if (lane == 0) islot[wave] = stop;
+  __syncthreads();
+  int istop = islot[0];
+  for (int q2 = 1; q2 < 4; ++q2) istop = islot[q2] < istop ? islot[q2] : istop;
+  if (tid >= istop) negkl = -__builtin_inf();
+  double v = negkl;
+  int bi = tid;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     const double ov = __shfl_xor(v, off);
-    const int oi = __shfl_xor(i, off);
-    if (ov > v || (ov == v && oi < i)) {
+    const int oi = __shfl_xor(bi, off);
+    if (ov > v || (ov == v && oi < bi)) {
       v = ov;
-      i = oi;
+      bi = oi;
     }
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
     red[wave] = v;
-    ired[wave] = i;
+    islot[4 + wave] = bi;
   }
   __syncthreads();
   double bv = red[0];
-  int bi = ired[0];
-  for (int q = 1; q < 4; ++q)
-    if (red[q] > bv || (red[q] == bv && ired[q] < bi)) {
-      bv = red[q];
-      bi = ired[q];
+  bi = islot[4];
+  for (int q2 = 1; q2 < 4; ++q2)
+    if (red[q2] > bv || (red[q2] == bv && islot[4 + q2] < bi)) {
+      bv = red[q2];
+      bi = islot[4 + q2];
     }
+  const bool ok = bv > -__builtin_inf();
+  if (ok && tid == bi) hbuf[0] = scale;
   __syncthreads();
-  *vbest = bv;
-  return bi;
+  if (ok && tid < nk) cvec[kidx[tid]] = irank[tid] <= bi ? cap : cc[tid] * hbuf[0];
+  __syncthreads();
+  if (ok && ai) *ci_io = cvec[row];
+  return ok;
 }
 
-__device__ __forceinline__ int block_min_int(int v, int* ired) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const int o = __shfl_xor(v, off);
-    v = o < v ? o : v;
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) ired[4 + wave] = v;
-  __syncthreads();
-  int r = ired[4];
-  for (int q = 5; q < 8; ++q) r = ired[q] < r ? ired[q] : r;
-  __syncthreads();
-  return r;
-}
-
-// a / b from the hardware reciprocal with one Newton step and one residual
-// correction (within an ulp or two; the twisted factorisation's pivots only)
-__device__ __forceinline__ double fdiv(double a, double b) {
-  double r = __builtin_amdgcn_rcp(b);
-  r = fma(fma(-b, r, 1.0), r, r);
-  const double q = a * r;
-  return fma(fma(-b, q, a), r, q);
-}
-
-template <int MODE>  // 0: filterL2, 1: ex_noregret
-__global__ void __launch_bounds__(256, 2) spectral_filter_kernel(FilterArgs A) {
+template <int MODE, bool DBG>  // MODE 0: filterL2, 1: ex_noregret; DBG: diagnostics of chunk 0
+__global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* uni = smem;                                     // 64 KB union
-  double* vec = reinterpret_cast<double*>(smem + FilterShared::kUnionBytes);
-  double* c = vec;                 // weights (active clients)
-  double* w = vec + 1 * FNP;       // normalised weights
-  double* sw = vec + 2 * FNP;      // sqrt(w)
-  double* gw = vec + 3 * FNP;      // G w
-  double* xv = vec + 4 * FNP;      // operator input (sw o vector)
-  double* yv = vec + 5 * FNP;      // G xv
-  double* rv = vec + 6 * FNP;      // Lanczos residual / scratch
-  double* uv = vec + 7 * FNP;      // Ritz vector (warm start)
-  double* tau = vec + 8 * FNP;     // outlier scores / Krum scores
-  double* sv = yv;                 // ex_noregret projection: weights in descending order
-  double* hl = xv;                 // ex_noregret projection: sv * log(sv / cap)
-  double* alpha = vec + 9 * FNP;   // [LMAX]
-  double* beta = alpha + LMAX;     // [LMAX]
-  double* beta2 = beta + LMAX;     // [LMAX] beta^2 (Sturm)
-  double* svec = beta2 + LMAX;     // [LMAX] eigenvector of T
-  double* hq = svec + LMAX;        // [LMAX] re-orthogonalisation coefficients
-  double* tcp = hq + LMAX;         // [LMAX] tridiagonal solve scratch
-  double* red = tcp + LMAX;        // [16]
-  double* scal = red + 16;         // [16] broadcast scalars
-  int* active = reinterpret_cast<int*>(scal + 16);  // [FNP]
-  int* kidx = active + FNP;                         // [FNP] compact -> client
-  int* irank = kidx + FNP;                          // [FNP] descending rank of compact entry
-  int* iscal = irank + FNP;                         // [16]
+  double* V = reinterpret_cast<double*>(smem);   // [LMAX][VST] Lanczos basis
+  double* xbuf = V + LMAX * VST;                 // [XLEN] operator input
+  double* rbuf = xbuf + XLEN;                    // [XLEN] residual before re-orthogonalisation
+  double* hbuf = rbuf + XLEN;                    // [64] Gram-Schmidt coefficients (+ |r'|^2)
+  double* red = hbuf + 64;                       // [2][16] block reductions (parity slots)
+  double* tri = red + 32;                        // [4][TRI] per-wave tridiagonal record
+  double* cvec = tri + 4 * TRI;                  // [FNP] weights (projection / final scale)
+  double* vscr = cvec + FNP;                     // [3][FNP] projection scratch
+  int* ibuf = reinterpret_cast<int*>(vscr + 3 * FNP);   // [3][FNP] int scratch + [16] argmax slots
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  const int row = tid >> 1;   // client row of this lane pair
+  const int half = tid & 1;   // which 64 columns of the row
+  const bool own = half == 0; // the even lane speaks for the pair
   const int n = A.n;
-  const int grow = tid >> 1;   // G row owned by this thread
-  const int ghalf = tid & 1;   // which 64 columns
-  const bool own = tid < FNP;  // thread owns client tid
+  double* trw = tri + wave * TRI;   // this wave's copy: alpha [0,64), beta^2 [64,128), s [128,192), scratch [192,256)
+  const int xi = row < 64 ? row : XOFF + row - 64;   // this row's slot in xbuf / rbuf
 
-  for (int chunk = blockIdx.x; chunk < A.nchunks; chunk += gridDim.x) {
-    const int64_t k0 = static_cast<int64_t>(chunk) * A.itv;
-    const int k = static_cast<int>((k0 + A.itv < A.d ? k0 + A.itv : A.d) - k0);
+  int rslot = 0;
+  // block sum of up to 4 owner contributions with one barrier (parity slots:
+  // a slot's reads happen before the barrier of the next reduction)
+  auto reduce4 = [&](double v0, double v1, double v2, double v3, double (&o)[4], int nv) __attribute__((always_inline)) {
+    // nv: how many of the four values are live (wave-uniform)
+    v0 = wave_sum(v0);
+    if (nv > 1) v1 = wave_sum(v1);
+    if (nv > 2) v2 = wave_sum(v2);
+    if (nv > 3) v3 = wave_sum(v3);
+    double* R = red + 16 * rslot;
+    if (lane == 0) {
+      R[4 * wave + 0] = v0;
+      if (nv > 1) R[4 * wave + 1] = v1;
+      if (nv > 2) R[4 * wave + 2] = v2;
+      if (nv > 3) R[4 * wave + 3] = v3;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nv) o[k] = (R[k] + R[4 + k]) + (R[8 + k] + R[12 + k]);
+    rslot ^= 1;
+  };
+  // first index of the largest v over the block (-inf for no candidate); one barrier
+  auto argmax_first = [&](double v, int i, double* vbest) __attribute__((always_inline)) -> int {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ov = __shfl_xor(v, off);
+      const int oi = __shfl_xor(i, off);
+      if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+      }
+    }
+    double* R = red + 16 * rslot;
+    int* I = ibuf + 3 * FNP + 8 * rslot;
+    if (lane == 0) {
+      R[wave] = v;
+      I[wave] = i;
+    }
+    __syncthreads();
+    double bv = R[0];
+    int bi = I[0];
+    for (int q = 1; q < 4; ++q)
+      if (R[q] > bv || (R[q] == bv && I[q] < bi)) {
+        bv = R[q];
+        bi = I[q];
+      }
+    rslot ^= 1;
+    *vbest = bv;
+    return bi;
+  };
 
-    // ================= Phase A: centred chunk Gram (fp64 MFMA) ==============
-    f64x4 acc[9];
-    if (wave == 0) filter_gram_phase<0>(A, k0, k, uni, acc);
-    else if (wave == 1) filter_gram_phase<1>(A, k0, k, uni, acc);
-    else if (wave == 2) filter_gram_phase<2>(A, k0, k, uni, acc);
-    else filter_gram_phase<3>(A, k0, k, uni, acc);
-
-    // ================= Phase B: G tiles -> registers (row layout) ===========
+  for (int ch = blockIdx.x; ch < A.nb; ch += gridDim.x) {
+    // ---- G rows into registers: lane pair (row, half) holds G[row][64 half + c]
     double g[64];
-    double* gbuf = reinterpret_cast<double*>(uni);  // [64 rows][128]
-#pragma unroll 1
-    for (int hh = 0; hh < 2; ++hh) {
+    {
+      const double2* Gr = reinterpret_cast<const double2*>(A.G + static_cast<size_t>(ch) * FNP * FNP + row * FNP +
+                                                           64 * half);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int tile = wave + 4 * t;
-        const int I = kFTileI[tile], J = kFTileJ[tile];
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          const int row = 16 * I + (lane >> 4) + 4 * rg;
-          const int col = 16 * J + (lane & 15);
-          const double v = acc[t][rg];
-          if ((row >> 6) == hh) gbuf[(row & 63) * FNP + col] = v;
-          if ((col >> 6) == hh) gbuf[(col & 63) * FNP + row] = v;
-        }
+      for (int c = 0; c < 32; ++c) {
+        const double2 v = Gr[c];
+        g[2 * c] = v.x;
+        g[2 * c + 1] = v.y;
       }
-      __syncthreads();
-      if ((grow >> 6) == hh) {
-#pragma unroll
-        for (int j = 0; j < 64; ++j) g[j] = gbuf[(grow & 63) * FNP + 64 * ghalf + j];
-      }
-      __syncthreads();
     }
-    const bool dbg = A.dbg != nullptr && chunk == 0;
-    if (dbg) {
-#pragma unroll
-      for (int j = 0; j < 64; ++j) A.dbg[grow * FNP + 64 * ghalf + j] = g[j];
-    }
-
-    // y = G x for x in LDS; every thread of the row pair gets the row value
-    auto gmv_row = [&](const double* x) -> double {
+    // y = G x for x in xbuf; both lanes of the pair get the row value
+    auto gmv = [&]() __attribute__((always_inline)) -> double {
+      const double2* xh = reinterpret_cast<const double2*>(xbuf + XOFF * half);
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-      const double* xh = x + 64 * ghalf;
 #pragma unroll
-      for (int j = 0; j < 64; j += 4) {
-        p0 += g[j] * xh[j];
-        p1 += g[j + 1] * xh[j + 1];
-        p2 += g[j + 2] * xh[j + 2];
-        p3 += g[j + 3] * xh[j + 3];
+      for (int c = 0; c < 32; c += 2) {
+        const double2 a = xh[c], b = xh[c + 1];
+        p0 = fma(g[2 * c], a.x, p0);
+        p1 = fma(g[2 * c + 1], a.y, p1);
+        p2 = fma(g[2 * c + 2], b.x, p2);
+        p3 = fma(g[2 * c + 3], b.y, p3);
+        // at most 8 x pieces in flight: the compiler would otherwise hoist all
+        // 32 loads (128 VGPRs beside the 128 of G) and spill
+        if ((c & 6) == 6) asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)::"memory");
       }
       const double p = (p0 + p1) + (p2 + p3);
-      return p + dpp_f64<0xB1>(p);   // the row's other half lives in lane ^ 1
-    };
-    // (C xv)[tid] for the owning threads, C = G - g1' - 1g' + s11' with
-    // g = gw, s = scal[0]; xv must be visible.  Two barriers.
-    auto cmul = [&]() -> double {
-      const double p = gmv_row(xv);
-      double a1 = own ? xv[tid] : 0.0;
-      double a2 = own ? gw[tid] * xv[tid] : 0.0;
-      a1 = wave_sum(a1);
-      a2 = wave_sum(a2);
-      if (lane == 0) {
-        red[wave] = a1;
-        red[4 + wave] = a2;
-      }
-      if (ghalf == 0) yv[grow] = p;
-      __syncthreads();
-      const double s1 = (red[0] + red[1]) + (red[2] + red[3]);
-      const double gy = (red[4] + red[5]) + (red[6] + red[7]);
-      const double r = own ? yv[tid] - gw[tid] * s1 - gy + scal[0] * s1 : 0.0;
-      __syncthreads();
-      return r;
+      return p + dpp_f64<0xB1>(p);
     };
 
-    // ============ ex_noregret: Krum pre-filter on the chunk =================
-    int n_keep = n;
-    double step = 0.0;
-    if constexpr (MODE == 1) {
-      const int fp = static_cast<int>(ceil(A.eps * n));
-      float* drow = reinterpret_cast<float*>(uni);   // [FNP][FNP] fp32 distances
-      {
-        double dg = 0.0;
-#pragma unroll
-        for (int j = 0; j < 64; ++j)
-          if (64 * ghalf + j == grow) dg = g[j];
-        if ((grow >> 6) == ghalf) xv[grow] = dg;
-      }
-      __syncthreads();
-      for (int j = 0; j < 64; ++j) {
-        const int col = 64 * ghalf + j;
-        if (grow < n && col < n) {
-          const double sq = xv[grow] + xv[col] - 2.0 * g[j];
-          drow[grow * FNP + col] = grow == col ? 0.f : static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
-        }
-      }
-      __syncthreads();
-      // each wave sorts whole rows (the n-1 off-diagonal distances, +inf
-      // padded to 128) with a register bitonic network, 2 elements per lane
-      for (int row = wave; row < n; row += 4) {
-        auto ld = [&](int e) -> float {
-          if (e >= n - 1) return __builtin_inff();
-          return drow[row * FNP + (e < row ? e : e + 1)];
-        };
-        float v0 = ld(2 * lane), v1 = ld(2 * lane + 1);
-#pragma unroll
-        for (int size = 2; size <= 128; size <<= 1) {
-#pragma unroll
-          for (int stride = size >> 1; stride >= 1; stride >>= 1) {
-            const bool asc = ((2 * lane) & size) == 0;
-            if (stride == 1) {
-              const float lo = fminf(v0, v1), hi = fmaxf(v0, v1);
-              v0 = asc ? lo : hi;
-              v1 = asc ? hi : lo;
-            } else {
-              const int ls = stride >> 1;
-              const float p0 = __shfl_xor(v0, ls), p1 = __shfl_xor(v1, ls);
-              const bool takemin = asc != ((lane & ls) != 0);
-              v0 = takemin ? fminf(v0, p0) : fmaxf(v0, p0);
-              v1 = takemin ? fminf(v1, p1) : fmaxf(v1, p1);
-            }
-          }
-        }
-        drow[row * FNP + 2 * lane] = v0;
-        drow[row * FNP + 2 * lane + 1] = v1;
-      }
-      __syncthreads();
-      // score = numpy pairwise fp32 sum of the m smallest (slice semantics)
-      const int m = n - fp - 2 >= 0 ? (n - fp - 2 < n - 1 ? n - fp - 2 : n - 1)
-                                    : ((n - 1) + (n - fp - 2) > 0 ? (n - 1) + (n - fp - 2) : 0);
-      if (tid < n) {
-        const float* row = drow + tid * FNP;
-        tau[tid] = static_cast<double>(np_pw32(m, [&](int q) { return row[q]; }));
-      }
-      __syncthreads();
-      // drop the fp largest scores (ties: later index dropped first)
-      if (own) {
-        int keep = 0;
-        if (tid < n) {
-          const double si = tau[tid];
-          int above = 0;
-          for (int j = 0; j < n; ++j) above += (tau[j] > si || (tau[j] == si && j > tid)) ? 1 : 0;
-          keep = above >= fp ? 1 : 0;
-        }
-        active[tid] = keep;
-      }
-      __syncthreads();
-      // compaction of the kept clients (client order)
-      if (own && active[tid]) {
-        int pos = 0;
-        for (int j = 0; j < tid; ++j) pos += active[j];
-        kidx[pos] = tid;
-      }
-      n_keep = n - (fp < n ? fp : n);
-      // max pairwise fp32 distance among kept clients
-      float md = 0.f;
-      for (int j = 0; j < 64; ++j) {
-        const int col = 64 * ghalf + j;
-        if (grow < n && col < n && grow < col && active[grow] && active[col]) {
-          const double sq = xv[grow] + xv[col] - 2.0 * g[j];
-          const float dd = static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
-          md = dd > md ? dd : md;
-        }
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const float o = __shfl_xor(md, off);
-        md = o > md ? o : md;
-      }
-      if (lane == 0) red[wave] = md;
-      __syncthreads();
-      float mdall = static_cast<float>(red[0]);
-      for (int q = 1; q < 4; ++q) mdall = static_cast<float>(red[q]) > mdall ? static_cast<float>(red[q]) : mdall;
-      __syncthreads();
-      step = static_cast<double>(0.5f / (mdall * mdall));
-      if (own) c[tid] = (tid < n && active[tid]) ? 1.0 : 0.0;
-      __syncthreads();
-    } else {
-      if (own) {
-        active[tid] = tid < n ? 1 : 0;
-        c[tid] = tid < n ? 1.0 : 0.0;
-      }
-      __syncthreads();
-    }
-
-    // ================= Phase C: iterations ==================================
-    const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n)
-                                : static_cast<int>(2 * A.eps * n_keep);
+    const bool dbg = DBG && ch == 0;
+    bool ai;     // this row is an active client
+    if constexpr (MODE == 1) ai = A.act[static_cast<size_t>(ch) * FNP + row] != 0;
+    else ai = row < n;
+    double ci = ai ? 1.0 : 0.0;
+    const int fdrop = static_cast<int>(ceil(A.eps * n));
+    const int n_keep = MODE == 1 ? n - (fdrop < n ? fdrop : n) : n;
+    const double step = MODE == 1 ? A.misc[static_cast<size_t>(ch) * kMisc + 1] : 0.0;
+    const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n) : static_cast<int>(2 * A.eps * n_keep);
+    double ui = 0.0;          // Ritz vector (warm start of the next iteration)
     bool have_u = false;
-    int m_hint = 0;   // Lanczos steps the previous iteration needed
-    double* V = reinterpret_cast<double*>(uni);   // [LMAX][VST] Lanczos basis
-    for (int it = 0; it < iters; ++it) {
-      // weights, G w, w'Gw, number of active clients
-      double csum = own && active[tid] ? c[tid] : 0.0;
-      csum = block_sum(csum, red);
-      double wi = 0.0;
-      if (own) {
-        wi = active[tid] ? c[tid] / csum : 0.0;
-        w[tid] = wi;
-        sw[tid] = sqrt(wi > 0.0 ? wi : 0.0);
-      }
-      __syncthreads();
-      {
-        const double p = gmv_row(w);
-        if (ghalf == 0) gw[grow] = p;
-      }
-      double sacc = 0.0, cnt = own && wi > 0.0 ? 1.0 : 0.0;
-      __syncthreads();
-      sacc = own ? wi * gw[tid] : 0.0;
-      block_sum2(sacc, cnt, red);
-      if (tid == 0) scal[0] = sacc;
-      const int nact = static_cast<int>(cnt);
-      __syncthreads();
+    int m_hint = 12;          // Lanczos steps the previous iteration needed
 
-      // ---- top eigenpair of M = W^1/2 C W^1/2: Lanczos, full reorth ----
-      const int msteps = nact < 1 ? 1 : (nact < LMAX ? nact : LMAX);
-      double lam = 0.0, resid_last = 0.0;
-      int rs_used = 0, m_last = 0;
-      long long tm[6] = {0, 0, 0, 0, 0, 0};   // cycle probes (diagnostics only)
-      long long t0c = clock64();
-#pragma unroll 1
-      for (int rs = 0; rs < LRESTART; ++rs) {
-        // start: warm Ritz vector (perturbed on a new outer iteration) or
-        // sqrt-weights times a fixed non-uniform pattern (sqrt-weights alone
-        // span the null vector: M W^1/2 1 = W^1/2 C w = 0)
-        double r0 = 0.0;
-        if (own && sw[tid] > 0.0) {
-          const double h = 0.5 + (tid * 0.6180339887498949 - floor(tid * 0.6180339887498949));
-          r0 = rs > 0 ? uv[tid] : (have_u ? uv[tid] + 1e-3 * sw[tid] * h : sw[tid] * h);
-        }
-        const double nrm = sqrt(block_sum(r0 * r0, red));
-        if (own) {
-          const double q = r0 / nrm;
-          V[tid] = q;
-          xv[tid] = sw[tid] * q;
-        }
-        __syncthreads();
-        int m = 0;
-        bool done = false;
-        double tscale = 0.0;
-        double theta_lb = -1e300;   // top Ritz value of the previous check
-        int next_check = m_hint > 8 ? m_hint : 8;
-        // Lanczos with deferred normalisation (3-4 barriers per step):
-        //   xv = W^1/2 rr, rr = beta_{j-1} q_j when `pend` (q_j not yet stored),
-        //   else rr = q_j.  One operator pass yields M rr, alpha_j and |rr|^2
-        //   together; full re-orthogonalisation by classical Gram-Schmidt with
-        //   a second pass only when the first removed more than half of |r|^2
-        //   (DGKS criterion, |r1|^2 = |r0|^2 - |h|^2).
-        bool pend = false;
-        double rr = own ? V[tid] : 0.0;
-        double r = 0.0;
-        double bprev = 0.0;
-        for (int j = 0; j < msteps; ++j) {
-          if (dbg) t0c = clock64();
-          // ---- (1) y = G xv with the sums for the centring, alpha and |rr|^2
-          {
-            const double p = gmv_row(xv);
-            double a1 = own ? xv[tid] : 0.0;
-            double a2 = own ? gw[tid] * xv[tid] : 0.0;
-            double a3 = ghalf == 0 ? xv[grow] * p : 0.0;
-            double a4 = own ? rr * rr : 0.0;
-            a1 = wave_sum(a1);
-            a2 = wave_sum(a2);
-            a3 = wave_sum(a3);
-            a4 = wave_sum(a4);
-            if (lane == 0) {
-              red[wave] = a1;
-              red[4 + wave] = a2;
-              red[8 + wave] = a3;
-              red[12 + wave] = a4;
-            }
-            if (ghalf == 0) yv[grow] = p;
-          }
-          __syncthreads();
-          if (dbg) { const long long t = clock64(); tm[0] += t - t0c; t0c = t; }
-          // ---- (2) r = M q_j - alpha_j q_j - beta_{j-1} q_{j-1}
-          double aj;
-          {
-            const double s1 = (red[0] + red[1]) + (red[2] + red[3]);
-            const double gy = (red[4] + red[5]) + (red[6] + red[7]);
-            const double xgx = (red[8] + red[9]) + (red[10] + red[11]);
-            const double nrm2 = (red[12] + red[13]) + (red[14] + red[15]);
-            const double bet = pend ? sqrt(nrm2) : 1.0;
-            if (pend) {
-              bprev = bet;
-              if (tid == 0) {
-                beta[j - 1] = bet;
-                beta2[j - 1] = bet * bet;
+    for (int it = 0; it < iters; ++it) {
+      const long long t_it = dbg ? clock64() : 0;
+      // ---- weights, g = G w, s = w^T G w, active count
+      double o[4];
+      reduce4(own && ai ? ci : 0.0, own && ai ? 1.0 : 0.0, 0.0, 0.0, o, 2);
+      const double csum = o[0];
+      const int nact = static_cast<int>(o[1]);
+      const double wi = ai ? ci / csum : 0.0;
+      const double swi = sqrt(wi > 0.0 ? wi : 0.0);
+      if (own) xbuf[xi] = wi;
+      __syncthreads();
+      const double gwi = gmv();
+      reduce4(own ? wi * gwi : 0.0, 0.0, 0.0, 0.0, o, 1);
+      const double sgw = o[0];
+
+      // ---- top eigenpair of M = W^1/2 C W^1/2: Lanczos with full re-orthogonalisation
+      double lam = 0.0, resid = 0.0;
+      int m_conv = 0, nchecks = 0, restarts = 0, passes2 = 0;
+      long long tph[4] = {0, 0, 0, 0};   // cycle probes (diagnostics only): check, matvec+alpha, dots, update
+      long long tq = 0;
+      double rt;   // unnormalised next basis vector (this row's entry)
+      {
+        // warm start from the previous Ritz vector (perturbed), else sqrt-weights
+        // times a fixed non-uniform pattern (sqrt-weights alone span M's null
+        // vector: M W^1/2 1 = W^1/2 C w = 0)
+        const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
+        rt = swi > 0.0 ? (have_u ? ui + 1e-3 * swi * hh : swi * hh) : 0.0;
+      }
+      for (;;) {   // explicit restarts from the Ritz vector when the basis is full
+        double xt = swi * rt;
+        if (own) xbuf[xi] = xt;
+        reduce4(own ? rt * rt : 0.0, own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, o, 3);
+        double nrm2 = o[0], S1 = o[1], GY = o[2];
+        double qprev = 0.0, tscale = 0.0, theta_lb = -1e300;
+        int next_check = m_hint - 3 > 4 ? m_hint - 3 : 4;
+        int m_a = -1;
+        double res_a = 0.0;
+        bool converged = false;
+        for (int j = 0;; ++j) {
+          const double bet = sqrt(nrm2);   // beta_{j-1} (the start norm at j = 0)
+          if (dbg) tq = clock64();
+          if (j > 0) {
+            if (lane == 0) trw[64 + j - 1] = bet * bet;
+            tscale = fmax(tscale, bet);
+            const bool breakdown = !(bet > 1e-14 * tscale);
+            if (breakdown || j >= nact || j == LMAX || j >= next_check) {
+              // ---- top eigenpair of T_j, identically in every wave
+              const int m = j;
+              ++nchecks;
+              __builtin_amdgcn_wave_barrier();
+              double lm, zlast;
+              tri_top(trw, m, tscale, theta_lb, &lm, &zlast);
+              lam = lm;
+              resid = fabs(bet * zlast);
+              theta_lb = lm;
+              if (resid <= kResTol * fabs(lm) || breakdown || j >= nact) {
+                converged = true;
+                m_conv = m;
+                break;
               }
-            }
-            aj = (xgx - 2.0 * s1 * gy + scal[0] * s1 * s1) / (bet * bet);
-            tscale = fmax(tscale, fabs(aj) + bprev);
-            if (own) {
-              const double q = rr / bet;
-              if (pend) V[j * VST + tid] = q;
-              r = sw[tid] * (yv[tid] - gw[tid] * s1 - gy + scal[0] * s1) / bet - aj * q;
-              if (j > 0) r -= bprev * V[(j - 1) * VST + tid];
-              rv[tid] = r;
+              if (j == LMAX) break;   // restart from the Ritz vector
+              // next check: extrapolate the residual's geometric decay
+              int adv = 4;
+              if (m_a >= 0 && res_a > resid && resid > 0.0) {
+                const double rate = log(resid / res_a) / (m - m_a);
+                const double need = log(kResTol * fabs(lm) / resid) / rate;
+                adv = need < 1.0 ? 1 : (need > 8.0 ? 8 : static_cast<int>(ceil(need)));
+              }
+              m_a = m;
+              res_a = resid;
+              next_check = m + adv;
             }
           }
-          __syncthreads();
-          if (dbg) { const long long t = clock64(); tm[1] += t - t0c; t0c = t; }
-          // ---- (3) re-orthogonalisation against q_0..q_j
-          double est2 = 0.0;   // |r|^2 after the last pass (Pythagoras)
+          if (dbg) { const long long t = clock64(); tph[0] += t - tq; tq = t; }
+          // ---- (1) y = G x~, M q_j = W^1/2 C x~ / beta, r' = M q_j - beta q_{j-1},
+          // alpha_j = q_j^T M q_j = x~^T C x~ / beta^2 (one block sum)
+          const double y = gmv();
+          const double cx = y - gwi * S1 - GY + sgw * S1;
+          const double ib = 1.0 / bet;
+          const double q = rt * ib;
+          if (own) V[j * VST + row] = q;
+          const double rp = swi * cx * ib - (j > 0 ? bet * qprev : 0.0);
+          if (own) rbuf[xi] = rp;
+          qprev = q;
+          reduce4(own ? swi * rt * y : 0.0, 0.0, 0.0, 0.0, o, 1);
+          const double aj = (o[0] - 2.0 * S1 * GY + sgw * S1 * S1) * (ib * ib);
+          // r'' = r' - alpha_j q_j before the re-orthogonalisation: without it the
+          // coefficients carry alpha_j and one classical pass loses ~3x of
+          // orthogonality per step (|r''| << |r'|)
+          double r = rp - aj * q;
+          double alpha = aj;
+          if (dbg) { const long long t = clock64(); tph[1] += t - tq; tq = t; }
 #pragma unroll 1
           for (int pass = 0; pass < 2; ++pass) {
+            // ---- (2) coefficients h_q = q_q . r (q <= j) and |r|^2 (first pass):
+            // 4 lanes per basis vector, 16-byte pieces interleaved; the first
+            // pass subtracts alpha_j q_j from r' on the fly
             {
-              // 4 lanes per basis vector, 16-byte chunks interleaved; slot
-              // j+1 is |r|^2 itself
               const int qq = tid >> 2, part = tid & 3;
-              double h0 = 0.0, h1 = 0.0;
-              if (qq <= j + 1) {
-                const double2* vq = reinterpret_cast<const double2*>(qq <= j ? V + qq * VST : rv) + part;
-                const double2* rp = reinterpret_cast<const double2*>(rv) + part;
+              const int top = pass == 0 ? j + 1 : j;
+              const double asub = pass == 0 ? aj : 0.0;
+              if (qq <= top) {
+                const bool isv = qq <= j;
+                const double* vb = V + (isv ? qq : 0) * VST;
+                const double* vj = V + j * VST;
+                double h0 = 0.0, h1 = 0.0;
 #pragma unroll
-                for (int e = 0; e < 64; e += 8) {
-                  const double2 a = vq[e], b = rp[e];
-                  const double2 c2 = vq[e + 4], d2 = rp[e + 4];
-                  h0 += a.x * b.x + a.y * b.y;
-                  h1 += c2.x * d2.x + c2.y * d2.y;
-                }
-              }
-              double h = h0 + h1;
-              h += dpp_f64<0xB1>(h);
-              h += dpp_f64<0x4E>(h);
-              if (part == 0 && qq <= j + 1) hq[qq] = h;
-            }
-            __syncthreads();
-            double hn2 = 0.0;
-            {
-              double u0 = 0.0, u1 = 0.0, u2 = 0.0, u3 = 0.0;
-              int qq = 0;
-              for (; qq + 3 <= j; qq += 4) {
-                const double c0 = hq[qq], c1 = hq[qq + 1], c2 = hq[qq + 2], c3 = hq[qq + 3];
-                hn2 += (c0 * c0 + c1 * c1) + (c2 * c2 + c3 * c3);
-                if (own) {
-                  u0 += c0 * V[qq * VST + tid];
-                  u1 += c1 * V[(qq + 1) * VST + tid];
-                  u2 += c2 * V[(qq + 2) * VST + tid];
-                  u3 += c3 * V[(qq + 3) * VST + tid];
-                }
-              }
-              for (; qq <= j; ++qq) {
-                const double c0 = hq[qq];
-                hn2 += c0 * c0;
-                if (own) u0 += c0 * V[qq * VST + tid];
-              }
-              if (own) r -= (u0 + u1) + (u2 + u3);
-            }
-            const double r02 = hq[j + 1];
-            est2 = r02 - hn2;
-            if (tid == 0) alpha[j] = pass == 0 ? aj + hq[j] : alpha[j] + hq[j];
-            // DGKS: a second pass only if the first removed over half of |r|^2
-            if (pass == 1 || !(est2 < 0.5 * r02)) break;
-            if (own) rv[tid] = r;
-            __syncthreads();
-          }
-          if (dbg) { const long long t = clock64(); tm[2] += t - t0c; t0c = t; }
-          m = j + 1;
-          const bool maybe_breakdown = !(est2 > 1e-26 * tscale * tscale);
-          const bool check = m == msteps || maybe_breakdown || m >= next_check;
-          if (!check) {
-            // deferred normalisation: the next step's operator pass measures |r|
-            if (own) {
-              rr = r;
-              xv[tid] = sw[tid] * r;
-            }
-            pend = true;
-            __syncthreads();
-            continue;
-          }
-          const double bj = sqrt(block_sum(own ? r * r : 0.0, red));
-          if (dbg) { const long long t = clock64(); tm[3] += t - t0c; t0c = t; }
-          if (tid == 0) {
-            beta[j] = bj;
-            beta2[j] = bj * bj;
-          }
-          const bool breakdown = !(bj > 1e-14 * tscale);
-          const bool last = m == msteps || breakdown;
-          {
-            __syncthreads();
-            // top eigenpair of T_m (wave 0, T in registers: lane q holds
-            // alpha_q, beta_q): multisection on Sturm counts, bracket from the
-            // previous check's Ritz value (interlacing: it only grows with m),
-            // then the eigenvector from a twisted factorisation
-            if (wave == 0) {
-              const double al = lane < m ? alpha[lane] : 0.0;
-              const double bl = lane + 1 < m ? beta[lane] : 0.0;
-              const double bp = (lane >= 1 && lane < m) ? beta[lane - 1] : 0.0;
-              const double rad = fabs(bp) + fabs(bl);
-              double lo = wave_min(lane < m ? al - rad : 1e300);
-              double hi = wave_max(lane < m ? al + rad : -1e300);
-              const double tiny = 1e-300 + 1e-30 * tscale;
-              // 64-point multisection on Sturm counts.  The count uses the
-              // division-free three-term recurrence of the leading principal
-              // minors p_q (d_q = p_q / p_{q-1} of the LDL^T pivots, same
-              // tiny-pivot rule), rescaled by exact powers of two every 4
-              // steps, so the dependent chain is one FMA per step.  With a
-              // previous Ritz value (a lower bound, interlacing) the first
-              // round's points are geometric above it, since the top value
-              // has moved little.
-              const bool geo = theta_lb > lo && theta_lb < hi;
-              if (geo) lo = theta_lb;
-              for (int round = 0; round < 16; ++round) {
-                const double fr = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, lane - 63)
-                                                      : (lane + 1) / 65.0;
-                const double x = lo + (hi - lo) * fr;
-                // alpha / beta^2 come from LDS at wave-uniform addresses (off
-                // the dependent chain); a zero minor keeps its sign bit (no
-                // division, so no tiny-pivot substitution is needed)
-                double p2 = 1.0;
-                double p1 = alpha[0] - x;
-                int cntb = __builtin_signbit(p1) ? 1 : 0;
-#pragma unroll 4
-                for (int q = 1; q < m; ++q) {
-                  const double pk = fma(alpha[q] - x, p1, -(beta2[q - 1] * p2));
-                  cntb += (__builtin_signbit(pk) ? 1 : 0) != (__builtin_signbit(p1) ? 1 : 0);
-                  p2 = p1;
-                  p1 = pk;
-                  if ((q & 3) == 3) {
-                    const int e = __builtin_amdgcn_frexp_exp(p1);
-                    p1 = __builtin_amdgcn_ldexp(p1, -e);
-                    p2 = __builtin_amdgcn_ldexp(p2, -e);
+                for (int e = 0; e < 16; e += 2) {
+                  const int i0 = 2 * (part + 4 * e), i1 = 2 * (part + 4 * (e + 1));
+                  const int r0 = i0 < 64 ? i0 : XOFF + i0 - 64, r1 = i1 < 64 ? i1 : XOFF + i1 - 64;
+                  const double2 b0 = *reinterpret_cast<const double2*>(rbuf + r0);
+                  const double2 c0 = *reinterpret_cast<const double2*>(vj + i0);
+                  const double2 b1 = *reinterpret_cast<const double2*>(rbuf + r1);
+                  const double2 c1 = *reinterpret_cast<const double2*>(vj + i1);
+                  const double s0x = fma(-asub, c0.x, b0.x), s0y = fma(-asub, c0.y, b0.y);
+                  const double s1x = fma(-asub, c1.x, b1.x), s1y = fma(-asub, c1.y, b1.y);
+                  double2 a0, a1;
+                  if (isv) {
+                    a0 = *reinterpret_cast<const double2*>(vb + i0);
+                    a1 = *reinterpret_cast<const double2*>(vb + i1);
+                  } else {
+                    a0 = double2{s0x, s0y};
+                    a1 = double2{s1x, s1y};
                   }
+                  h0 = fma(a0.x, s0x, fma(a0.y, s0y, h0));
+                  h1 = fma(a1.x, s1x, fma(a1.y, s1y, h1));
+                  if ((e & 2) == 2) asm volatile("" : "+v"(h0), "+v"(h1)::"memory");
                 }
-                const unsigned long long ok = __builtin_amdgcn_ballot_w64(cntb >= m);
-                const int first = ok ? __builtin_ctzll(ok) : 64;
-                const double flo = first == 0 ? 0.0
-                                              : ((geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 64)
-                                                                     : first / 65.0);
-                const double fhi = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 63)
-                                                       : (first + 1) / 65.0;
-                const double nlo = lo + (hi - lo) * flo;
-                const double nhi = first < 64 ? lo + (hi - lo) * fhi : hi;
-                lo = nlo;
-                hi = nhi;
-                if (hi - lo <= 2e-16 * fmax(fabs(lo), fabs(hi))) break;
-              }
-              if (dbg) tm[5] += clock64() - t0c;
-              const double lm = 0.5 * (lo + hi);
-              // twisted factorisation of T - lm I: forward pivots dp, backward dm
-              double dpv = 0.0, dmv = 0.0;
-              {
-                double dp = readlane_f64(al, 0) - lm;
-                if (fabs(dp) < tiny) dp = -tiny;
-                dpv = writelane_f64(dp, 0, dpv);
-                for (int q = 1; q < m; ++q) {
-                  dp = (alpha[q] - lm) - fdiv(beta2[q - 1], dp);
-                  if (fabs(dp) < tiny) dp = -tiny;
-                  dpv = writelane_f64(dp, q, dpv);
-                }
-                double dm = readlane_f64(al, m - 1) - lm;
-                if (fabs(dm) < tiny) dm = -tiny;
-                dmv = writelane_f64(dm, m - 1, dmv);
-                for (int q = m - 2; q >= 0; --q) {
-                  dm = (alpha[q] - lm) - fdiv(beta2[q], dm);
-                  if (fabs(dm) < tiny) dm = -tiny;
-                  dmv = writelane_f64(dm, q, dmv);
-                }
-              }
-              // twist index: smallest |gamma_q| = |dp_q + dm_q - (alpha_q - lm)|
-              double gam = lane < m ? fabs(dpv + dmv - (al - lm)) : 1e308;
-              int tw = lane;
-#pragma unroll
-              for (int off = 32; off >= 1; off >>= 1) {
-                const double og = __shfl_xor(gam, off);
-                const int ot = __shfl_xor(tw, off);
-                if (og < gam || (og == gam && ot < tw)) {
-                  gam = og;
-                  tw = ot;
-                }
-              }
-              tw = __builtin_amdgcn_readfirstlane(tw);
-              // z_tw = 1; z_q = -(b_q / dp_q) z_{q+1} below, z_{q+1} = -(b_q / dm_{q+1}) z_q above
-              const double dmn = __shfl_down(dmv, 1);
-              const double fdown = lane < m ? -bl / dpv : 0.0;
-              const double fup = lane + 1 < m ? -bl / dmn : 0.0;
-              double zv = lane == tw ? 1.0 : 0.0;
-              double z = 1.0;
-              for (int q = tw - 1; q >= 0; --q) {
-                z *= readlane_f64(fdown, q);
-                zv = writelane_f64(z, q, zv);
-              }
-              z = 1.0;
-              for (int q = tw; q + 1 < m; ++q) {
-                z *= readlane_f64(fup, q);
-                zv = writelane_f64(z, q + 1, zv);
-              }
-              if (lane >= m) zv = 0.0;
-              const double amax = wave_max(fabs(zv));
-              const double zs = zv / amax;
-              const double nn = amax * sqrt(wave_sum(zs * zs));
-              zv = zv / nn;
-              if (lane < m) svec[lane] = zv;
-              if (lane == 0) {
-                scal[1] = lm;
-                scal[2] = fabs(bj * readlane_f64(zv, m - 1));
+                double h = h0 + h1;
+                h += dpp_f64<0xB1>(h);
+                h += dpp_f64<0x4E>(h);
+                if (part == 0) hbuf[qq] = h;
               }
             }
             __syncthreads();
-            lam = scal[1];
-            resid_last = scal[2];
-            theta_lb = lam;
-            next_check = m + 8;
-            if (dbg) { const long long t = clock64(); tm[4] += t - t0c; t0c = t; }
-            done = last || resid_last <= 1e-13 * fabs(lam);
-            if (done) break;
+            if (dbg) { const long long t = clock64(); tph[2] += t - tq; tq = t; }
+            // ---- (3) r -= sum_q h_q q_q: the lane pair splits q = 0..j into two
+            // contiguous halves, 4 coefficients per batch (loads issued together)
+            double hn2 = 0.0, upd = 0.0;
+            {
+              const int nq = j + 1, hq0 = (nq + 1) >> 1;
+              const int qlo = half ? hq0 : 0, qhi = half ? nq : hq0;
+              double u[4] = {0.0, 0.0, 0.0, 0.0}, e2[4] = {0.0, 0.0, 0.0, 0.0};
+              int qq = qlo;
+              for (; qq + 4 <= qhi; qq += 4) {
+                double hv[4], vv[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                  hv[t] = hbuf[qq + t];
+                  vv[t] = V[(qq + t) * VST + row];
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                  u[t] = fma(hv[t], vv[t], u[t]);
+                  e2[t] = fma(hv[t], hv[t], e2[t]);
+                }
+              }
+              for (; qq < qhi; ++qq) {
+                const double hv = hbuf[qq];
+                u[0] = fma(hv, V[qq * VST + row], u[0]);
+                e2[0] = fma(hv, hv, e2[0]);
+              }
+              upd = (u[0] + u[1]) + (u[2] + u[3]);
+              hn2 = (e2[0] + e2[1]) + (e2[2] + e2[3]);
+              upd += dpp_f64<0xB1>(upd);
+              hn2 += dpp_f64<0xB1>(hn2);
+            }
+            r -= upd;
+            alpha += hbuf[j];
+            if (pass == 1) break;
+            const double rr2 = hbuf[j + 1];
+            if (!(rr2 - hn2 < kDgks * rr2)) break;
+            // heavy cancellation: one more classical Gram-Schmidt pass
+            ++passes2;
+            if (own) rbuf[xi] = r;
+            __syncthreads();
           }
-          if (own) {
-            const double qn = r / bj;
-            V[(j + 1) * VST + tid] = qn;
-            xv[tid] = sw[tid] * qn;
-            rr = qn;
+          if (lane == 0) trw[j] = alpha;
+          tscale = fmax(tscale, fabs(alpha));
+          // ---- (4) next unnormalised vector and its sums (deferred normalisation)
+          rt = r;
+          xt = swi * r;
+          if (own) xbuf[xi] = xt;
+          reduce4(own ? r * r : 0.0, own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, o, 3);
+          nrm2 = o[0];
+          S1 = o[1];
+          GY = o[2];
+          if (dbg) { const long long t = clock64(); tph[3] += t - tq; tq = t; }
+        }
+        // ---- Ritz vector u = V s
+        {
+          const int m = converged ? m_conv : LMAX;
+          double u0 = 0.0, u1 = 0.0;
+          int qq = 0;
+          for (; qq + 1 < m; qq += 2) {
+            u0 = fma(trw[128 + qq], V[qq * VST + row], u0);
+            u1 = fma(trw[128 + qq + 1], V[(qq + 1) * VST + row], u1);
           }
-          pend = false;
-          bprev = bj;
-          __syncthreads();
+          if (qq < m) u0 = fma(trw[128 + qq], V[qq * VST + row], u0);
+          ui = u0 + u1;
         }
-        // Ritz vector
-        if (own) {
-          double u = 0.0;
-          for (int q = 0; q < m; ++q) u += V[q * VST + tid] * svec[q];
-          uv[tid] = u;
-        }
-        m_last = m;
-        rs_used = rs + 1;
-        m_hint = m;
-        __syncthreads();
-        if (m >= nact || resid_last <= 1e-13 * fabs(lam)) break;
+        if (converged || restarts == kMaxRestarts) break;
+        ++restarts;
+        rt = ui;
+        __syncthreads();   // every wave's reads of V before the restart overwrites it
       }
+      m_hint = m_conv > 4 ? m_conv : 4;
       have_u = true;
       if (dbg && it < 256) {
         double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
-        if (own) rec[tid] = c[tid];
+        if (own) rec[row] = ci;
         if (tid == 0) {
           rec[FNP] = lam;
-          rec[FNP + 1] = m_last;
-          rec[FNP + 2] = resid_last;
-          rec[FNP + 3] = rs_used;
+          rec[FNP + 1] = m_conv;
+          rec[FNP + 2] = resid;
+          rec[FNP + 3] = nchecks;
           rec[FNP + 4] = nact;
-          rec[FNP + 5] = scal[0];
-          for (int q = 0; q < 6; ++q) rec[FNP + 6 + q] = static_cast<double>(tm[q]);
+          rec[FNP + 5] = sgw;
+          rec[FNP + 6] = restarts;
+          rec[FNP + 7] = passes2;
+          rec[FNP + 8] = static_cast<double>(clock64() - t_it);
+          for (int k = 0; k < 4; ++k) rec[FNP + 9 + k] = static_cast<double>(tph[k]);
         }
       }
-      // ---- early exit (robust_estimator.py:164 / :70) ----
+      // ---- early exit (robust_estimator.py:163-164 / :71-72)
       if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
-      // ---- tau_j = ((x_j - mu).v)^2 = (C W^1/2 u)_j^2 / lam ----
-      if (own) xv[tid] = sw[tid] * uv[tid];
-      __syncthreads();
-      const double cu = cmul();
-      const double ti = own ? cu * cu / lam : 0.0;
+      // ---- tau_j = ((x_j - mu).v)^2 = (C W^1/2 u)_j^2 / lambda
+      {
+        const double xt = swi * ui;
+        if (own) xbuf[xi] = xt;
+        reduce4(own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, 0.0, o, 2);
+      }
+      const double cu = gmv() - gwi * o[0] - o[1] + sgw * o[0];
+      const double ti = cu * cu / lam;
       if constexpr (MODE == 0) {
-        // c *= 1 - tau/tau_max; drop argmax (first index); c /= |c|_1
+        // c *= 1 - tau/tau_max; drop the argmax (first index); c /= |c|_1
         double tmax = 0.0;
-        const int p = block_argmax_first(own && active[tid] ? ti : -__builtin_inf(), tid, red,
-                                         reinterpret_cast<int*>(iscal), &tmax);
-        double cn = 0.0;
-        if (own && active[tid] && tid != p) cn = c[tid] * (1.0 - ti / tmax);
-        const double l1 = block_sum(fabs(cn), red);
-        if (own) {
-          c[tid] = cn / l1;
-          if (tid == p) active[tid] = 0;
-        }
-        __syncthreads();
+        const int p = argmax_first(own && ai ? ti : -__builtin_inf(), row, &tmax);
+        const double cn = (ai && row != p) ? ci * (1.0 - ti / tmax) : 0.0;
+        reduce4(own ? fabs(cn) : 0.0, 0.0, 0.0, 0.0, o, 1);
+        ci = cn / o[0];
+        if (row == p) ai = false;
       } else {
-        // c *= 1 - step*tau, then the KL projection onto
-        // {sum c = 1, c <= cap} (robust_estimator.py:77-99)
+        // c *= 1 - step*tau, then the KL projection onto {sum c = 1, c <= cap}
+        // (robust_estimator.py:74-99) over the n_keep kept clients
         const int nk = n_keep;
         const double cap = 1.0 / (1.0 - A.eps) / nk;
-        if (own && active[tid]) c[tid] = c[tid] * (1.0 - step * ti);
-        __syncthreads();
-        double* cc = rv;   // compacted weights
-        if (tid < nk) cc[tid] = c[kidx[tid]];
-        __syncthreads();
-        // descending rank; ties: later compact index first (flip of a
-        // stable ascending order)
-        if (tid < nk) {
-          const double v = cc[tid];
-          int rk = 0;
-          for (int q = 0; q < nk; ++q) rk += (cc[q] > v || (cc[q] == v && q > tid)) ? 1 : 0;
-          irank[tid] = rk;
-          sv[rk] = v;
-          hl[rk] = v * log(v / cap);
-        }
-        __syncthreads();
-        // candidate i caps the i+1 largest at cap and rescales the rest
-        double negkl = -__builtin_inf(), scale = 0.0;
-        int stop = 1 << 30;
-        if (tid < nk) {
-          const int i = tid;
-          const double clip = 1.0 - np_pw64(0, i + 1, [&](int) { return cap; });
-          if (clip <= 0.0) {
-            stop = i;
-          } else if (i + 1 < nk) {
-            const double norm = np_pw64(i + 1, nk - i - 1, [&](int q) { return sv[q]; });
-            scale = clip / norm;
-            if (!(sv[i + 1] * scale > cap)) {
-              double head = 0.0;
-              for (int q = 0; q <= i; ++q) head += hl[q];
-              negkl = -(head - norm * log(scale));
-            }
-          }
-        }
-        const int istop = block_min_int(stop, reinterpret_cast<int*>(iscal));
-        if (tid >= istop) negkl = -__builtin_inf();
-        double best = 0.0;
-        const int bi = block_argmax_first(negkl, tid, red, reinterpret_cast<int*>(iscal), &best);
-        if (!(best > -__builtin_inf())) {
+        if (ai) ci = ci * (1.0 - step * ti);
+        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf)) {
           if (tid == 0) *A.status = 2;   // projected_c None -> TypeError in the reference
           break;
         }
-        if (tid == bi) scal[3] = scale;
-        __syncthreads();
-        if (tid < nk) c[kidx[tid]] = irank[tid] <= bi ? cap : cc[tid] * scal[3];
-        __syncthreads();
       }
     }
 
-    // ================= Phase D: weighted mean over the chunk ================
-    {
-      if (tid == 0) {
-        // np.average's scale: pairwise sum of the kept weights in order
-        int q = 0;
-        for (int i = 0; i < n; ++i)
-          if (active[i]) rv[q++] = c[i];
-        scal[4] = np_pw64(0, q, [&](int z) { return rv[z]; });
-      }
-      __syncthreads();
-      const double cs = scal[4];
-      for (int cc2 = tid; cc2 < k; cc2 += 256) {
-        double s = 0.0;
-        for (int i = 0; i < n; ++i)
-          if (active[i]) s += static_cast<double>(A.X[static_cast<int64_t>(i) * A.ldx + k0 + cc2]) * c[i];
-        A.out[k0 + cc2] = s / cs;
-      }
-      __syncthreads();
+    // ---- final weights and np.average's scale (pairwise sum of the kept weights in order)
+    __syncthreads();
+    if (own) {
+      cvec[row] = ai ? ci : 0.0;
+      ibuf[2 * FNP + row] = ai ? 1 : 0;
+      A.c[static_cast<size_t>(ch) * FNP + row] = ai ? ci : 0.0;
+      A.act[static_cast<size_t>(ch) * FNP + row] = ai ? 1 : 0;
     }
+    __syncthreads();
+    if (tid == 0) {
+      int q2 = 0;
+      double* kept = vscr;
+      for (int i = 0; i < n; ++i)
+        if (ibuf[2 * FNP + i]) kept[q2++] = cvec[i];
+      A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int z) { return kept[z]; });
+    }
+    __syncthreads();
   }
 }
 
-size_t filter_lds_bytes() {
-  return FilterShared::kUnionBytes + sizeof(double) * (9 * FNP + 6 * LMAX + 32) + sizeof(int) * (3 * FNP + 16);
+// ============================================================================
+// chunk_mean_kernel: the weighted mean of every coordinate of the batch
+// ============================================================================
+__global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                                         int itv, int64_t chunk0, int nb,
+                                                         const double* __restrict__ c, const int* __restrict__ act,
+                                                         const double* __restrict__ misc, double* __restrict__ out) {
+  const int64_t j0 = chunk0 * itv;
+  const int64_t jend = (chunk0 + nb) * static_cast<int64_t>(itv);
+  const int64_t j1 = jend < d ? jend : d;
+  const int64_t j = j0 + static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= j1) return;
+  const int b = static_cast<int>((j - j0) / itv);
+  const double* cb = c + static_cast<size_t>(b) * FNP;
+  const int* ab = act + static_cast<size_t>(b) * FNP;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i)
+    if (ab[i]) s += static_cast<double>(X[static_cast<int64_t>(i) * ldx + j]) * cb[i];
+  out[j] = s / misc[static_cast<size_t>(b) * kMisc];
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+constexpr size_t kChunkWsBytes = sizeof(double) * (FNP * FNP + FNP + kMisc) + sizeof(int) * FNP;
+
+size_t filter_workspace_bytes(int64_t d, int itv) {
+  const int64_t nchunks = cdiv(d, itv);
+  const int64_t b = nchunks < kBatch ? nchunks : kBatch;
+  return static_cast<size_t>(b) * kChunkWsBytes + 256;
 }
 
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
-                  double expansion, double* out, int* status, double* dbg, hipStream_t s) {
+                  double expansion, double* out, int* status, double* dbg, void* ws, size_t ws_bytes,
+                  hipStream_t s) {
   SRA_REQUIRE(n >= 1 && n <= FNP, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", FNP, n);
   SRA_REQUIRE(itv >= 1, SRA_ERR_ARG, "itv must be >= 1");
   const int64_t nchunks = cdiv(d, itv);
   SRA_REQUIRE(nchunks < (int64_t(1) << 31), SRA_ERR_ARG, "too many chunks");
-  FilterArgs a{X, n, d, ldx, itv, static_cast<int>(nchunks), eps, sigma, expansion, out, status, dbg};
-  const size_t lds = filter_lds_bytes();
-  const int grid = static_cast<int>(nchunks < 512 ? nchunks : 512);
-  if (mode == 0) {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&spectral_filter_kernel<0>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL(spectral_filter_kernel<0>, dim3(grid), dim3(256), lds, s, a);
-  } else {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&spectral_filter_kernel<1>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL(spectral_filter_kernel<1>, dim3(grid), dim3(256), lds, s, a);
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= filter_workspace_bytes(d, itv), SRA_ERR_WORKSPACE,
+              "filter workspace too small: need %zu bytes", filter_workspace_bytes(d, itv));
+  const int64_t bmax = nchunks < kBatch ? nchunks : kBatch;
+  char* base = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  double* Gws = reinterpret_cast<double*>(base);
+  double* cws = Gws + static_cast<size_t>(bmax) * FNP * FNP;
+  double* mws = cws + static_cast<size_t>(bmax) * FNP;
+  int* aws = reinterpret_cast<int*>(mws + static_cast<size_t>(bmax) * kMisc);
+  const void* solve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<0, true>)
+                                       : reinterpret_cast<const void*>(&filter_solve_kernel<0, false>))
+                                : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
+                                       : reinterpret_cast<const void*>(&filter_solve_kernel<1, false>));
+  SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
+  for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
+    const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
+    GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws};
+    hipLaunchKernelGGL(chunk_gram_kernel, dim3(nb), dim3(256), 0, s, ga);
+    int rc = launch_status("chunk_gram_kernel");
+    if (rc) return rc;
+    if (dbg != nullptr && c0 == 0)
+      SRA_HIP(hipMemcpyAsync(dbg, Gws, sizeof(double) * FNP * FNP, hipMemcpyDeviceToDevice, s));
+    if (mode == 1) {
+      PreArgs pa{Gws, aws, mws, n, nb, eps};
+      hipLaunchKernelGGL(noregret_pre_kernel, dim3(nb), dim3(256), 0, s, pa);
+      rc = launch_status("noregret_pre_kernel");
+      if (rc) return rc;
+    }
+    SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr};
+    const int grid = nb < 512 ? nb : 512;
+    if (mode == 0 && dbg) hipLaunchKernelGGL((filter_solve_kernel<0, true>), dim3(grid), dim3(256), kSolveLds, s, sa);
+    else if (mode == 0) hipLaunchKernelGGL((filter_solve_kernel<0, false>), dim3(grid), dim3(256), kSolveLds, s, sa);
+    else if (dbg) hipLaunchKernelGGL((filter_solve_kernel<1, true>), dim3(grid), dim3(256), kSolveLds, s, sa);
+    else hipLaunchKernelGGL((filter_solve_kernel<1, false>), dim3(grid), dim3(256), kSolveLds, s, sa);
+    rc = launch_status("filter_solve_kernel");
+    if (rc) return rc;
+    const int64_t jend = (c0 + nb) * static_cast<int64_t>(itv);
+    const int64_t ncols = (jend < d ? jend : d) - c0 * static_cast<int64_t>(itv);
+    hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws,
+                       aws, mws, out);
+    rc = launch_status("chunk_mean_kernel");
+    if (rc) return rc;
   }
-  return launch_status("spectral_filter_kernel");
+  return SRA_OK;
 }
 
-}  // namespace sra
-
-extern "C" int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
-                              double eps, double sigma, double expansion, double* out, int32_t* status,
-                              void* stream) {
+static int filter_checks(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, double eps, double* out,
+                         int32_t* status) {
   SRA_REQUIRE(X != nullptr && out != nullptr && status != nullptr, SRA_ERR_ARG, "null pointer");
   SRA_REQUIRE(d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad d/ldx");
   SRA_REQUIRE(mode == 0 || mode == 1, SRA_ERR_ARG, "mode must be 0 (filterL2) or 1 (ex_noregret)");
@@ -996,18 +1086,37 @@ extern "C" int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx,
   // distances of the rest: the reference raises (amax of an empty list) below 2
   SRA_REQUIRE(mode == 0 || n - static_cast<int64_t>(std::ceil(eps * n)) >= 2, SRA_ERR_ARG,
               "ex_noregret needs at least 2 clients after dropping ceil(eps*n)");
-  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status,
-                            nullptr, static_cast<hipStream_t>(stream));
+  // f = ceil(eps*n) = 0: argpartition(metric, -0)[:-0] keeps nothing and the
+  // reference's np.amax of the empty distance list raises ValueError
+  SRA_REQUIRE(mode == 0 || std::ceil(eps * n) >= 1.0, SRA_ERR_ARG,
+              "ex_noregret with ceil(eps*n) = 0 keeps no client (the reference raises ValueError)");
+  return SRA_OK;
+}
+
+}  // namespace sra
+
+extern "C" int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && d >= 1 && itv >= 1, SRA_ERR_SHAPE, "bad shape");
+  *bytes = sra::filter_workspace_bytes(d, itv);
+  return SRA_OK;
+}
+
+extern "C" int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
+                              double eps, double sigma, double expansion, double* out, int32_t* status, void* ws,
+                              size_t ws_bytes, void* stream) {
+  const int rc = sra::filter_checks(X, n, d, ldx, mode, eps, out, status);
+  if (rc) return rc;
+  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, nullptr,
+                            ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
                                     double eps, double sigma, double expansion, double* out, int32_t* status,
-                                    double* dbg, void* stream) {
-  SRA_REQUIRE(X != nullptr && out != nullptr && status != nullptr && dbg != nullptr, SRA_ERR_ARG, "null pointer");
-  SRA_REQUIRE(d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad d/ldx");
-  SRA_REQUIRE(mode == 0 || mode == 1, SRA_ERR_ARG, "mode must be 0 (filterL2) or 1 (ex_noregret)");
-  SRA_REQUIRE(mode == 0 || n - static_cast<int64_t>(std::ceil(eps * n)) >= 2, SRA_ERR_ARG,
-              "ex_noregret needs at least 2 clients after dropping ceil(eps*n)");
-  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, dbg,
-                            static_cast<hipStream_t>(stream));
+                                    double* dbg, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(dbg != nullptr, SRA_ERR_ARG, "null pointer");
+  const int rc = sra::filter_checks(X, n, d, ldx, mode, eps, out, status);
+  if (rc) return rc;
+  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, dbg, ws,
+                            ws_bytes, static_cast<hipStream_t>(stream));
 }

@@ -28,11 +28,21 @@ def as_matrix(X):
         raise TypeError("engine ops compute in float32, got %s" % X.dtype)
     if X.dim() != 2:
         raise ValueError("expected an (N, d) matrix, got shape %s" % (tuple(X.shape),))
-    if X.shape[1] > 1 and X.stride(1) != 1:
-        X = X.contiguous()
+    X = _unit_rows(X)
     n, d = X.shape
     ldx = X.stride(0) if n > 1 else d
-    return X, int(n), int(d), int(max(ldx, d))
+    return X, int(n), int(d), int(ldx)
+
+
+def _unit_rows(X):
+    """A view the kernels can walk as rows[i * ldx + j]: unit column stride and
+    non-overlapping rows (ldx >= d).  Expanded (stride 0) or overlapping views
+    (unfold / as_strided) would make the kernels read past the real storage,
+    so they are copied."""
+    n, d = X.shape
+    if (d > 1 and X.stride(1) != 1) or (n > 1 and X.stride(0) < d):
+        X = X.contiguous()
+    return X
 
 
 def _out(X, d, out):
@@ -176,6 +186,24 @@ def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
     return (out, sel) if selected else out
 
 
+def bulyan_coordinates(A, beta, median_index=False, median_row=False):
+    """The per-coordinate Bulyan stage over the columns of a (theta, d) float64
+    device matrix (robust_estimator.py:259-275 for every column): returns the
+    (d,) float64 means, plus the median indices (int64) and distance rows
+    ((theta, d) float64) when asked."""
+    if not isinstance(A, torch.Tensor) or not A.is_cuda or A.dtype != torch.float64 or A.dim() != 2:
+        raise TypeError("bulyan_coordinates takes a (theta, d) float64 CUDA tensor")
+    A = _unit_rows(A)
+    theta, d = A.shape
+    lda = A.stride(0) if theta > 1 else d
+    out = torch.empty(d, dtype=torch.float64, device=A.device)
+    mi = torch.empty(d, dtype=torch.int64, device=A.device) if median_index else None
+    mr = torch.empty((theta, d), dtype=torch.float64, device=A.device) if median_row else None
+    _lib.call("sra_bulyan_coordinate_f64", A.data_ptr(), int(theta), int(d), int(lda), int(beta), out.data_ptr(),
+              mi.data_ptr() if mi is not None else None, mr.data_ptr() if mr is not None else None, int(d),
+              _stream_ptr(A.device))
+    return out, mi, mr
+
 # ---------------------------------------------------------------------------
 # spectral filters
 # ---------------------------------------------------------------------------
@@ -194,8 +222,11 @@ def _filter(X, mode, eps, sigma, expansion, itv, check):
     X, n, d, ldx = as_matrix(X)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
     status = torch.zeros(1, dtype=torch.int32, device=X.device)
-    _lib.call("sra_filter_f32", X.data_ptr(), n, d, ldx, int(mode), chunk_width(d, itv), float(eps), float(sigma),
-              float(expansion), out.data_ptr(), status.data_ptr(), _stream_ptr(X.device))
+    w = chunk_width(d, itv)
+    nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_filter_f32", X.data_ptr(), n, d, ldx, int(mode), w, float(eps), float(sigma),
+              float(expansion), out.data_ptr(), status.data_ptr(), ws.data_ptr(), nb, _stream_ptr(X.device))
     if check and int(status.item()) == 2:
         raise TypeError("ex_noregret: no feasible capped-simplex projection (projected_c is None)")
     return out
@@ -206,15 +237,19 @@ FILTER_DEBUG_DOUBLES = 128 * 128 + 256 * 144
 
 def filter_debug(X, mode, eps, sigma, expansion, itv):
     """Run a filter and return (out, G0, records) for chunk 0: G0 the centred
-    chunk Gram (n x n fp64), records an (iters, 144) array of
-    [weights(128), lambda, lanczos_steps, ritz_residual, restarts, 12 solver scalars]."""
+    chunk Gram (n x n fp64), records an (iters, 144) array of [weights(128),
+    lambda, lanczos_steps, ritz_residual, checks, active, w'Gw, restarts,
+    second_gs_passes, cycles, 7 unused]."""
     X, n, d, ldx = as_matrix(X)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
     status = torch.zeros(1, dtype=torch.int32, device=X.device)
     dbg = torch.full((FILTER_DEBUG_DOUBLES,), float("nan"), dtype=torch.float64, device=X.device)
-    _lib.call("sra_filter_debug_f32", X.data_ptr(), n, d, ldx, int(mode), chunk_width(d, itv), float(eps),
+    w = chunk_width(d, itv)
+    nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_filter_debug_f32", X.data_ptr(), n, d, ldx, int(mode), w, float(eps),
               float(sigma), float(expansion), out.data_ptr(), status.data_ptr(), dbg.data_ptr(),
-              _stream_ptr(X.device))
+              ws.data_ptr(), nb, _stream_ptr(X.device))
     dbg = dbg.cpu()
     G = dbg[:128 * 128].reshape(128, 128)[:n, :n].clone()
     recs = dbg[128 * 128:].reshape(256, 144)
@@ -267,11 +302,10 @@ def as_rows(X):
         raise TypeError("clipping ops take float32 or float64 rows, got %s" % X.dtype)
     if X.dim() != 2:
         raise ValueError("expected a (k, d) matrix, got shape %s" % (tuple(X.shape),))
-    if X.shape[1] > 1 and X.stride(1) != 1:
-        X = X.contiguous()
+    X = _unit_rows(X)
     k, d = X.shape
     ld = X.stride(0) if k > 1 else d
-    return X, int(k), int(d), int(max(ld, d))
+    return X, int(k), int(d), int(ld)
 
 
 def window_means(X, stride, width, nwin, out=None):

@@ -116,7 +116,11 @@ def krum_(samples, f):
     _, scores = engine.krum_select(st.X, f, 1, scores=True)
     if st.device_io:
         return scores
-    return [np.float32(v) for v in scores.cpu().numpy()]
+    # numpy returns float64 metrics for float64 rows (an attack's promoted rows,
+    # attack.py:197/260); the distances themselves are the fp32 Gram route's
+    # (near-tie picks can differ from float64 BLAS norms)
+    typ = np.dtype(st.np_dtype).type
+    return [typ(v) for v in scores.cpu().numpy()]
 
 
 def krum(samples, f):
@@ -138,6 +142,37 @@ def mom_krum(samples, f, bucket_size=3):
 # ---------------------------------------------------------------------------
 # Bulyan
 # ---------------------------------------------------------------------------
+def _coord64(arr):
+    """One coordinate's values as a (theta, 1) float64 device column; returns
+    (column, device_io)."""
+    if isinstance(arr, torch.Tensor):
+        col = arr.reshape(-1, 1).to(dtype=torch.float64)
+        io = arr.is_cuda
+        return (col if io else col.to(_device())).contiguous(), io
+    a = np.asarray(arr, dtype=np.float64).reshape(-1, 1)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(_device()), False
+
+
+def bulyan_median(arr):
+    """robust_estimator.py:259-270: (index of the value with the smallest total
+    distance to the others -- np.argmin of numpy's pairwise row sums, the first
+    NaN if any -- and that value's float64 distance row)."""
+    col, io = _coord64(arr)
+    _, mi, mr = engine.bulyan_coordinates(col, 0, median_index=True, median_row=True)
+    if io:
+        return mi[0], mr[:, 0]
+    return np.int64(mi.cpu()[0]), mr[:, 0].cpu().numpy()
+
+
+def bulyan_one_coordinate(arr, beta):
+    """robust_estimator.py:272-275: mean of arr[np.argsort(distances)[:beta]]
+    (Python slice semantics for beta < 0; equal distances take the smaller
+    value first -- numpy's unstable argsort leaves that order undefined)."""
+    col, io = _coord64(arr)
+    out, _, _ = engine.bulyan_coordinates(col, int(beta))
+    return out[0] if io else np.float64(out.cpu()[0])
+
+
 def bulyan(grads, f, aggsubfunc="trimmedmean"):
     """robust_estimator.py:277-332 (float64 result, like the reference)."""
     st = _stage(grads)

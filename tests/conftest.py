@@ -53,7 +53,7 @@ def load_fixture(path):
 def fixtures(prefix=None, func=None):
     out = []
     for p in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
-        if os.path.basename(p).startswith(("c1_", "dispatch_", "attack_", "dba_")):
+        if os.path.basename(p).startswith(("c1_", "dispatch_", "attack_", "dba_", "bulyan_coord")):
             continue
         rec = load_fixture(p)
         if prefix and not rec["name"].startswith(prefix):

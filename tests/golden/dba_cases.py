@@ -50,6 +50,11 @@ CASES = {
     # FoolsGold (helper.py:291-325, 1321-1417): updates carry per-layer gradient LISTS; SGD step on the model
     "foolsgold_n24": ("foolsgold_update", {}, 24, 5, {"fg_use_memory": False}, 2),
     "foolsgold_mem_n24": ("foolsgold_update", {}, 24, 5, {"fg_use_memory": True}, 2),
+    # 2f < N < 4f: beta < 0, torch slicing [:beta] drops -beta values (keep 0 -> mean of nothing, NaN)
+    "bulyankrum_n30_f8_negbeta": ("bulyan_krum", {"f": 8}, 30, 8, {}, 1),
+    "bulyanmedian_n30_f8_negbeta": ("bulyan_median", {"f": 8}, 30, 8, {}, 1),
+    "bulyantrimmed_n40_f12_negbeta": ("bulyan_trimmed_mean", {"f": 12}, 40, 12, {}, 1),
+    "bulyanmedian_n30_f10_negbeta": ("bulyan_median", {"f": 10}, 30, 10, {}, 1),
 }
 
 BASE_PARAMS = {"eta": 1, "sharding": False, "shard_size": 0.2, "adversary_list": [0, 1, 2, 3, 4],

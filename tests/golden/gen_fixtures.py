@@ -130,6 +130,13 @@ def main():
         for mode in ("krum", "median", "trimmedmean"):
             cases.append(("bulyan_%s_n%d_f%d" % (mode, n, f), "bulyan", {"f": f, "aggsubfunc": mode}, xs,
                           (lambda xs=xs, f=f, mode=mode: ref.bulyan(xs, f, aggsubfunc=mode))))
+    # 2f < N < 4f: beta = theta - 2f < 0, so argsort(...)[:beta] drops -beta values
+    # from the far end (Python slice semantics); keep 0 is the mean of an empty slice
+    for n, f, shp, seed in [(30, 8, (60,), 46), (40, 12, (55,), 47), (30, 10, (20,), 48)]:
+        xs = make_clients(n, shp, seed, byz=f)
+        for mode in ("krum", "median", "trimmedmean"):
+            cases.append(("bulyan_%s_n%d_f%d_negbeta" % (mode, n, f), "bulyan", {"f": f, "aggsubfunc": mode}, xs,
+                          (lambda xs=xs, f=f, mode=mode: ref.bulyan(xs, f, aggsubfunc=mode))))
     xs = make_clients(10, (5,), 45)
     cases.append(("bulyan_theta0", "bulyan", {"f": 5, "aggsubfunc": "trimmedmean"}, xs,
                   (lambda xs=xs: ref.bulyan(xs, 5, aggsubfunc="trimmedmean"))))
@@ -156,8 +163,70 @@ def main():
         cases.append(("mom_ex_noregret_%s" % tag, "mom_ex_noregret", params, xs,
                       (lambda xs=xs, p=params: ref.mom_ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"], p["delta"]))))
 
+    only = sys.argv[1:]   # optional name filters: regenerate only matching fixtures
+    # ex_noregret with ceil(eps*n) = 0: argpartition(..., -0)[:-0] keeps nothing -> ValueError
+    xs = make_clients(20, (30,), 54, byz=3)
+    p0 = {"eps": 0.0, "sigma": 0.02, "expansion": 20, "itv": 15}
+    cases.append(("ex_noregret_f0", "ex_noregret", p0, xs,
+                  (lambda xs=xs, p=p0: ref.ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+
+    # ---- BASELINE configs at their client counts (a few chunks / columns of d) ----
+    # C3 bulyan N=128 f=20 (theta 88, beta 48); C4 filterl2 / ex_noregret N=128 with
+    # simulate.py's eps = malnum/nworker = 0.2, sigma 1e-5, itv 1000; C5 mom_filterL2
+    # N=512 with delta = e^-26 (128 buckets of 4)
+    xs = make_clients(128, (1500,), 80, byz=20)
+    for mode in ("median", "trimmedmean", "krum"):
+        cases.append(("bulyan_%s_n128_f20_c3" % mode, "bulyan", {"f": 20, "aggsubfunc": mode}, xs,
+                      (lambda xs=xs, mode=mode: ref.bulyan(xs, 20, aggsubfunc=mode))))
+    pc4 = {"eps": 0.2, "sigma": 1e-5, "expansion": 20, "itv": 1000}
+    xs = make_clients(128, (1300,), 81, byz=20)
+    cases.append(("filterL2_n128_c4", "filterL2", pc4, xs,
+                  (lambda xs=xs, p=pc4: ref.filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+    cases.append(("ex_noregret_n128_c4", "ex_noregret", pc4, xs,
+                  (lambda xs=xs, p=pc4: ref.ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+    pc5 = dict(pc4, delta=float(np.exp(-26)))
+    xs = make_clients(512, (1200,), 82, byz=100)
+    cases.append(("mom_filterL2_n512_c5", "mom_filterL2", pc5, xs,
+                  (lambda xs=xs, p=pc5: ref.mom_filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"],
+                                                         p["delta"]))))
+
     for name, func, params, xs, call in cases:
+        if only and not any(o in name for o in only):
+            continue
         run_case(ref, name, func, params, xs, call)
+    # ---- the scalar Bulyan helpers (robust_estimator.py:259-275) -------------
+    if not only or any(o in "bulyan_coord" for o in only):
+        rng = np.random.default_rng(49)
+        arrs, betas = [], []
+        for theta, kind in [(1, "n"), (2, "n"), (7, "n"), (10, "n"), (60, "n"), (88, "n"), (100, "n"), (13, "int"),
+                            (40, "int"), (20, "nan"), (24, "nan0"), (16, "inf"), (130, "n"), (200, "int")]:
+            a = rng.standard_normal(theta).astype(np.float32).astype(np.float64)
+            if kind == "int":
+                a = rng.integers(-3, 4, size=theta).astype(np.float64)
+            elif kind == "nan":
+                a[5] = np.nan
+            elif kind == "nan0":
+                a[0] = np.nan
+            elif kind == "inf":
+                a[3] = np.inf
+            for beta in sorted({theta - 40, theta // 2, -3, 0, theta, theta + 5, 1}):
+                arrs.append(a)
+                betas.append(beta)
+        mi, rows, one = [], [], []
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            for a, beta in zip(arrs, betas):
+                m, row = ref.bulyan_median(a)
+                mi.append(int(m))
+                rows.append(np.asarray(row, dtype=np.float64))
+                one.append(float(ref.bulyan_one_coordinate(a, beta)))
+        flat = np.concatenate(arrs)
+        lens = np.array([len(a) for a in arrs])
+        np.savez(os.path.join(HERE, "bulyan_coord.npz"), values=flat, lens=lens, betas=np.array(betas),
+                 median_index=np.array(mi), rows=np.concatenate(rows), one=np.array(one))
+        print("wrote bulyan_coord (%d cases)" % len(arrs))
+    if only:
+        return
 
     # ---- C1 plumbing: one round of the ConvNet layers at N=100 ------------
     seed = 70

@@ -56,7 +56,7 @@ def test_golden_bulyan(rec):
 
 
 @pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
-@pytest.mark.parametrize("n,f", [(100, 20), (64, 10), (37, 8)])
+@pytest.mark.parametrize("n,f", [(100, 20), (64, 10), (37, 8), (100, 30), (30, 8)])
 def test_bulyan_against_oracle(mode, n, f):
     x = make_rows(n, 1500, seed=77 + n + f, byz=f)
     want, _ = _leftfirst_and_ties(list(x), f, mode)
@@ -80,3 +80,27 @@ def test_bulyan_even_theta_tiebreak_dense_ties():
         want, _ = _leftfirst_and_ties(list(x), 10, mode)
         got = engine.bulyan(torch.from_numpy(x).cuda(), 10, mode).cpu().numpy()
         np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)
+
+
+def test_scalar_helpers_match_reference():
+    """Drop-in bulyan_median / bulyan_one_coordinate (robust_estimator.py:259-275)
+    against the live-reference fixture (float64 in, numpy scalars out)."""
+    import os
+    import warnings
+    from conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "bulyan_coord.npz"))
+    offs = np.concatenate([[0], np.cumsum(z["lens"])])
+    for c in range(len(z["lens"])):
+        a = z["values"][offs[c]:offs[c + 1]]
+        beta = int(z["betas"][c])
+        m, row = gre.bulyan_median(a)
+        assert int(m) == int(z["median_index"][c])
+        np.testing.assert_array_equal(row, z["rows"][offs[c]:offs[c + 1]])
+        got = gre.bulyan_one_coordinate(a, beta)
+        assert isinstance(got, np.float64)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            want = orc.bulyan_one_coordinate_leftfirst(a, beta)
+        np.testing.assert_allclose(got, want, rtol=1e-15, atol=0)
+        if not orc.bulyan_boundary_tie(a, beta):
+            np.testing.assert_allclose(got, z["one"][c], rtol=1e-15, atol=0)

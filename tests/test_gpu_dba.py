@@ -101,8 +101,18 @@ def test_sharded_median_matches_oracle_bit_exact():
     np.testing.assert_array_equal(got.astype(np.float32), od.median(od.sharding(x, random)))
 
 
+def _near(cand, ref, atol, rtol):
+    """Per coordinate: some candidate equals ref within tolerance (NaN matches NaN:
+    keep = 0 when beta <= -theta is the mean of an empty slice)."""
+    close = np.abs(cand - ref[None, :]) <= atol + rtol * np.abs(ref)
+    both_nan = np.isnan(cand) & np.isnan(ref)[None, :]
+    return (close | both_nan).any(axis=0)
+
+
 @pytest.mark.parametrize("name", ["bulyankrum_n24_f5", "bulyankrum_n25_f2", "bulyanmedian_n25_f5",
-                                  "bulyanmedian_n24_f5", "bulyantrimmed_n25_f5"])
+                                  "bulyanmedian_n24_f5", "bulyantrimmed_n25_f5", "bulyankrum_n30_f8_negbeta",
+                                  "bulyanmedian_n30_f8_negbeta", "bulyantrimmed_n40_f12_negbeta",
+                                  "bulyanmedian_n30_f10_negbeta"])
 def test_bulyan(name):
     method, kw, *_ = CASES[name]
     mode = {"bulyan_krum": "krum", "bulyan_median": "median", "bulyan_trimmed_mean": "trimmedmean"}[method]
@@ -112,8 +122,8 @@ def test_bulyan(name):
     np.testing.assert_allclose(got, od.bulyan(x, SEG, kw["f"], mode).astype(np.float32), rtol=0, atol=0)
     cand = od.bulyan_candidates(x, SEG, kw["f"], mode)
     ref = fx(name)["out_0"].astype(np.float64)
-    assert (np.abs(cand - ref[None, :]) <= 1e-7 + 2e-6 * np.abs(ref)).any(axis=0).all()
-    assert (np.abs(cand - got[None, :]) <= 1e-7 + 2e-6 * np.abs(got)).any(axis=0).all()
+    assert _near(cand, ref, 1e-7, 2e-6).all()
+    assert _near(cand, got.astype(np.float64), 1e-7, 2e-6).all()
 
 
 def test_bulyan_krum_f1_rejected_and_theta():

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 from conftest import fixtures, gpu_available
+from test_oracle_golden import FILTER_C4_ATOL
 from oracle import robust_np as orc
 from synth import make_rows
 
@@ -50,6 +51,10 @@ def test_golden_filters(rec):
     got = call(xs, rec["params"])
     assert got.dtype == np.float64 and got.shape == rec["out"].shape
     rtol, atol = TOL[rec["func"]]
+    if rec["func"] in ("filterL2", "mom_filterL2") and rec["name"].endswith(("_c4", "_c5")):
+        # the reference's own fp64 error amplification over 50 iterations
+        # (tests/test_oracle_golden.py, FILTER_C4_ATOL)
+        rtol, atol = 0.0, FILTER_C4_ATOL * np.abs(rec["out"]).max()
     np.testing.assert_allclose(got, rec["out"], rtol=rtol, atol=atol)
 
 
@@ -82,8 +87,11 @@ def test_filter_chunks_independent_and_full_size_smoke():
     np.testing.assert_array_equal(whole, np.concatenate([a, b]))
     g = torch.Generator(device="cuda").manual_seed(1)
     Y = 0.01 * torch.randn(128, 1_000_000, device="cuda", generator=g)
-    out = engine.filter_l2(Y, 0.2, 1e-5, 20, 1000)
-    assert torch.isfinite(out).all()
+    out = engine.filter_l2(Y, 0.2, 1e-5, 20, 1000).cpu().numpy()
+    assert np.isfinite(out).all()
+    # benign-only data: the hardest case for the eigensolver (clustered spectrum)
+    want = orc.filterL2(list(Y[:, 999_000:].cpu().numpy()), 0.2, 1e-5, 20, 1000)
+    np.testing.assert_allclose(out[999_000:], want, rtol=0, atol=FILTER_C4_ATOL * np.abs(want).max())
 
 
 def test_filter_internals_chunk0():
@@ -97,3 +105,65 @@ def test_filter_internals_chunk0():
     np.testing.assert_allclose(G.numpy(), want, rtol=1e-10, atol=1e-14 * np.abs(want).max())
     lam0 = np.linalg.eigvalsh(z.T @ z / x.shape[0])[-1]
     assert abs(float(recs[0, 128]) - lam0) <= 1e-10 * lam0
+
+
+def test_ex_noregret_f0_raises():
+    """ceil(eps*n) = 0 keeps no client: the reference raises ValueError."""
+    x = make_rows(20, 30, seed=3, byz=3)
+    with pytest.raises(ValueError):
+        engine.ex_noregret(torch.from_numpy(x).cuda(), 0.0, 0.02, 20, 15)
+
+
+# ---- BASELINE configs at full size: chunks are independent, so the device
+# result over the whole layer must equal the oracle on any chunk ----------------
+SIM = dict(eps=0.2, sigma=1e-5, expansion=20, itv=1000)   # simulate.py defaults (SURVEY §8 convention)
+
+
+def _device_rows(n, d, byz, seed):
+    """N x d fp32 on the device: 0.01 N(0,1) + 0.001 N(0,1) drift, rows < byz
+    at -10x the benign mean (+ noise), like tests/golden/synth.py."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    drift = torch.empty(d, dtype=torch.float32, device="cuda").normal_(0, 0.001, generator=g)
+    for r0 in range(0, n, 16):
+        X[r0:r0 + 16].normal_(0, 0.01, generator=g).add_(drift)
+    if byz:
+        mean = X[byz:].double().mean(0)
+        X[:byz] = (-10.0 * mean).float()[None, :] + 0.001 * torch.randn(byz, d, device="cuda", generator=g)
+    return X
+
+
+def _chunk_check(X, got, chunks, oracle_fn, atol_of_max):
+    for c in chunks:
+        lo, hi = c * 1000, min((c + 1) * 1000, X.shape[1])
+        xs = list(X[:, lo:hi].cpu().numpy())
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            want = oracle_fn(xs)
+        np.testing.assert_allclose(got[lo:hi], want, rtol=0, atol=atol_of_max * np.abs(want).max())
+
+
+def test_c4_filterl2_fullsize_chunks():
+    """C4: filterl2, N=128 x d=1e7, against the oracle on 3 chunks."""
+    X = _device_rows(128, 10_000_000, 20, seed=41)
+    got = engine.filter_l2(X, **SIM).cpu().numpy()
+    assert np.isfinite(got).all()
+    _chunk_check(X, got, [0, 4321, 9999], lambda xs: orc.filterL2(xs, **SIM), FILTER_C4_ATOL)
+
+
+def test_c4_ex_noregret_fullsize_chunks():
+    """C4: ex_noregret, N=128 x d=1e7 (eps = malnum/nworker = 0.2), against the oracle on 3 chunks."""
+    X = _device_rows(128, 10_000_000, 20, seed=42)
+    got = engine.ex_noregret(X, **SIM).cpu().numpy()
+    assert np.isfinite(got).all()
+    _chunk_check(X, got, [0, 5678, 9999], lambda xs: orc.ex_noregret(xs, **SIM), 2e-5)
+
+
+def test_c5_mom_filterl2_per_gpu_shard_chunks():
+    """C5 per GPU: mom_filterl2, N=512 x d=1.25e7, delta = e^-26 (128 buckets of 4),
+    against the oracle on 2 chunks."""
+    delta = float(np.exp(-26))
+    X = _device_rows(512, 12_500_000, 100, seed=43)
+    got = engine.mom_filter_l2(X, delta=delta, **SIM).cpu().numpy()
+    assert np.isfinite(got).all()
+    _chunk_check(X, got, [0, 12499], lambda xs: orc.mom_filterL2(xs, delta=delta, **SIM), FILTER_C4_ATOL)

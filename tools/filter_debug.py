@@ -31,32 +31,40 @@ for it in range(recs.shape[0]):
     r = recs[it].numpy()
     if np.isnan(r[128]) and np.isnan(r[0]):
         break
-    print("it", it, "lam", r[128], "m", r[129], "resid", r[130], "rs", r[131], "c", r[:min(n, 8)])
-    print("    scal4..15", r[132:144])
+    print("it", it, "lam", r[128], "m", r[129], "resid", r[130], "checks", r[131], "nact", r[132],
+          "restarts", r[134], "gs2", r[135], "cycles", r[136], "c", r[:min(n, 8)])
 print("out", out.cpu().numpy()[:8])
 print("want", z["out"].ravel()[:8] if "out" in z else None)
 
 if len(sys.argv) > 2 and sys.argv[2] == "synthetic":
+    import time
     for mode in (0, 1):
         g = torch.Generator(device="cuda").manual_seed(1)
         Y = 0.01 * torch.randn(128, 1000, device="cuda", generator=g)
         out, G, recs = engine.filter_debug(Y, mode, 0.2, 1e-5, 20, 1000)
-        ms, rss = [], []
+        ms, ck, p2, cyc = [], [], [], []
         for it in range(recs.shape[0]):
             r = recs[it].numpy()
             if np.isnan(r[128]):
                 break
             ms.append(int(r[129]))
-            rss.append(int(r[131]))
-        print("mode", mode, "iters", len(ms), "steps", ms, "restarts", rss)
+            ck.append(int(r[131]))
+            p2.append(int(r[135]))
+            cyc.append(r[136])
+        print("mode", mode, "iters", len(ms), "lanczos steps", sum(ms), ms)
+        print("   checks", sum(ck), "second GS passes", sum(p2), "restarts", int(recs[:len(ms), 134].sum()))
         print("   resid", [float("%.1e" % recs[i, 130]) for i in range(len(ms))][:10])
-        tsum = recs[:len(ms), 134:140].numpy().sum(0)
-        print("   cycles cmul/aj/reorth/beta/check(multisection part) per step:", (tsum / max(1, sum(ms))).round(0), "total Mcyc", tsum[:5].sum() / 1e6)
-        torch.cuda.synchronize()
-        import time
-        t0 = time.perf_counter()
-        for _ in range(3):
-            engine.filter_l2(Y, 0.2, 1e-5, 20, 1000, check=False) if mode == 0 else \
-                engine.ex_noregret(Y, 0.2, 1e-5, 20, 1000, check=False)
-        torch.cuda.synchronize()
-        print("   one chunk: %.3f ms" % ((time.perf_counter() - t0) / 3 * 1e3))
+        print("   Mcycles/iteration %.3f, cycles per Lanczos step %.0f" % (np.mean(cyc) / 1e6, sum(cyc) / max(1, sum(ms))))
+        ph = recs[:len(ms), 137:141].numpy().sum(0)
+        print("   per step: check %.0f  matvec+alpha %.0f  dots %.0f  update+reduce %.0f cycles" % tuple(ph / max(1, sum(ms))))
+        for d in (1000, 10_000_000):
+            Z = 0.01 * torch.randn(128, d, device="cuda", generator=g)
+            fn = engine.filter_l2 if mode == 0 else engine.ex_noregret
+            fn(Z, 0.2, 1e-5, 20, 1000, check=False)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                fn(Z, 0.2, 1e-5, 20, 1000, check=False)
+            torch.cuda.synchronize()
+            print("   d=%d: %.3f ms" % (d, (time.perf_counter() - t0) / 3 * 1e3))
+            del Z
