@@ -347,11 +347,18 @@ def bulyan(grads, f, aggsubfunc="trimmedmean"):
 # ----------------------------------------------------------------------------
 # spectral filters
 # ----------------------------------------------------------------------------
-def _weighted_cov(centered, c):
+def _weighted_cov(centered, c, order="gemm"):
+    """The weighted covariance of robust_estimator.py:158; ``order="reverse"``
+    sums the clients' outer products in reverse client order instead (the same
+    mathematics in another fp64 evaluation order, used to measure how far the
+    reference's own result moves under rounding: tests/test_gpu_filters.py)."""
+    if order == "reverse":
+        z, w = centered[::-1], c[::-1]
+        return (z.T * w) @ z / w.sum()
     return (centered.T * c) @ centered / c.sum()
 
 
-def filterL2_(samples, eps=0.2, sigma=1, expansion=20):
+def filterL2_(samples, eps=0.2, sigma=1, expansion=20, order="gemm"):
     """robust_estimator.py:144-177 on one (n, k) chunk (primal k x k form)."""
     x = np.asarray(samples)
     n0, k = x.shape
@@ -359,7 +366,7 @@ def filterL2_(samples, eps=0.2, sigma=1, expansion=20):
     for _ in range(2 * int(eps * n0)):
         mu = np.average(x, axis=0, weights=c)
         z = x - mu
-        lam, vec = eigh(_weighted_cov(z, c), subset_by_index=[k - 1, k - 1])
+        lam, vec = eigh(_weighted_cov(z, c, order), subset_by_index=[k - 1, k - 1])
         lam = lam[0]
         if lam * lam <= expansion * sigma * sigma:
             return mu
@@ -381,15 +388,15 @@ def _chunked(samples, itv, fn):
     return np.concatenate(out, axis=0).reshape(shape)
 
 
-def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV):
+def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, order="gemm"):
     """robust_estimator.py:180-208: filterL2_ over itv-wide chunks."""
-    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion))
+    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion, order))
 
 
-def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
+def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30), order="gemm"):
     """robust_estimator.py:210-218."""
     num, size = bucket_count(len(samples), eps, delta)
-    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv)
+    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv, order)
 
 
 def kl_capped_projection(c, eps):

@@ -54,7 +54,7 @@ constexpr int VST = 136;           // basis row stride (doubles): the 4 rows one
 constexpr int XOFF = 66;           // vector buffers: entries [64, 128) start at XOFF (bank-disjoint halves)
 constexpr int XLEN = XOFF + 64 + 2;
 constexpr int TRI = 256;           // per-wave tridiagonal record: alpha[64] beta^2[64] s / dp[64] dm[64]
-constexpr double kResTol = 1e-13;  // converged when the Ritz residual <= kResTol * lambda
+constexpr double kResTol = 1e-16;  // converged when the Ritz residual <= kResTol * lambda
 constexpr double kDgks = 0.5;      // second Gram-Schmidt pass when |r|^2 < kDgks * |r'|^2 (DGKS)
 constexpr int kMaxRestarts = 8;
 constexpr int kBatch = 8192;       // chunks per workspace batch
@@ -752,7 +752,7 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
         reduce4(own ? rt * rt : 0.0, own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, o, 3);
         double nrm2 = o[0], S1 = o[1], GY = o[2];
         double qprev = 0.0, tscale = 0.0, theta_lb = -1e300;
-        int next_check = m_hint - 3 > 4 ? m_hint - 3 : 4;
+        int next_check = m_hint - 1 > 4 ? m_hint - 1 : 4;
         int m_a = -1;
         double res_a = 0.0;
         bool converged = false;
