@@ -16,11 +16,14 @@
 // (and after real NaNs), so positions 0..n-1 of the padded sort are exactly
 // numpy's sorted column.
 //
-// Roofline: HBM-bound, 4*N*d + 4*d bytes per call.  At N=128 the network is
-// ~1.5k compare-exchanges per coordinate (~3k VALU lane-ops), below the
-// ~6.7k lane-ops per coordinate the VALU affords at 6 TB/s.
+// Roofline: HBM-bound, 4*N*d + 4*d bytes per call.  The exact-N trimmed mean
+// at N=128 (select_plain_kernel) runs a network pruned to the kept ranks
+// (network_fast); its VALU instruction count per tile is reported by
+// tools/isa_stats.py and set against the HBM time in DESIGN.md §3.
 //
-// N > 128 (e.g. the N=512 MoM/8-GPU config) uses an LDS bitonic path.
+// 128 < N <= 512 (the N=512 MoM / 8-GPU config) uses 2 or 4 lanes per
+// coordinate with DPP bitonic merges (select_quad_kernel); larger N, or row
+// strides beyond 32-bit lane offsets, fall back to an LDS bitonic tile.
 #include "sra_common.hpp"
 
 #include <algorithm>
@@ -297,320 +300,6 @@ __global__ void __launch_bounds__(256) select_plain_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
-// LDS-DMA path (exact N = NX, NX % 4 == 0, NX <= 128): persistent waves, one per
-// SIMD (a 256-thread workgroup per CU).  Each wave owns a private LDS tile of
-// NX rows x 64 coordinates (NX*256 bytes, 32 KiB at N=128) and walks the column
-// tiles t = wave, wave + W, ... :
-//   1. wait for tile t's LDS-DMA (s_waitcnt vmcnt(0): the wave's only VMEM
-//      operations in flight are that DMA and the previous tile's store);
-//   2. read its column into VGPRs (ds_read, lane = coordinate: conflict-free);
-//   3. issue the DMA of tile t+W into the same buffer -- NX/4
-//      global_load_lds_dwordx4, 1 KiB each (4 rows x 256 B, coalesced) -- so the
-//      HBM fetch of the next tile runs under
-//   4. the NaN check, the selection network and the ascending-order sum of
-//      tile t (the same code as select_reg_kernel: bit-identical results).
-// The fetch is decoupled from the register file (no VGPRs hold in-flight
-// data), so the wave never waits on HBM once the pipeline is primed and the
-// column's ~3k VALU ops overlap the next tile's 32 KiB fetch completely.
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-// One global_load_lds_dwordx4: 64 lanes x 16 B from the wave-uniform row base
-// `rows4` (SGPR pair) + each lane's 32-bit byte offset into LDS at
-// lds_base + I*1024 (M0 is set and restored inside the statement; hipcc does
-// not count asm loads -- the kernel waits with an explicit vmcnt(0)).
-template <int I>
-__device__ __forceinline__ void dma16(uint64_t rows4, unsigned lane_off, uint32_t lds_base) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %4\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep) : "v"(lane_off), "s"(rows4), "s"(lds_base), "i"(I * 1024) : "memory");
-}
-
-template <int... I>
-__device__ __forceinline__ void dma_rows(uint64_t p, uint64_t step4, unsigned lane_off, uint32_t lds_base,
-                                         std::integer_sequence<int, I...>) {
-  // a running SGPR row pointer (opaque to the optimiser, so it is not
-  // rematerialised as NX/4 hoisted 64-bit offsets)
-  ((dma16<I>(p, lane_off, lds_base), p += step4, opaque_sgpr(p)), ...);
-}
-
-// tile t = columns [64t, 64t+64) of all NX rows -> the wave's LDS tile
-template <int NX>
-__device__ __forceinline__ void dma_tile(const float* X, int64_t t, uint64_t step4, unsigned lane_off,
-                                         uint32_t lds_base) {
-  const uint64_t a = reinterpret_cast<uint64_t>(X + t * kWave);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-  dma_rows((static_cast<uint64_t>(hi) << 32) | lo, step4, lane_off, lds_base,
-           std::make_integer_sequence<int, NX / 4>{});
-}
-
-template <int MODE, int NX, int BX>
-__global__ void __launch_bounds__(256, 1) select_dma_kernel(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
-                                                           float* __restrict__ out) {
-  static_assert(NX % 4 == 0 && NX <= 128, "exact-N DMA path");
-  extern __shared__ __attribute__((aligned(16))) float lds_tiles[];
-  constexpr int P = ((NX + 15) / 16) * 16;
-  constexpr int P2 = next_pow2(P);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const unsigned lane = threadIdx.x & 63u;
-  float* buf = lds_tiles + wave * (NX * kWave);
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)buf);
-  const int64_t ldb = ldx * 4;
-  const uint64_t step4 = static_cast<uint64_t>(ldb) * 4;
-  const unsigned lane_off = static_cast<unsigned>((lane >> 4) * ldb) + (lane & 15u) * 16u;
-  const int64_t step = static_cast<int64_t>(gridDim.x) * 4;
-  int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + wave;
-  if (t >= ntiles) return;
-  dma_tile<NX>(X, t, step4, lane_off, lds_base);
-
-  constexpr int kMedLo = (NX - 1) / 2;
-  constexpr int kMedHi = NX / 2;
-  constexpr int kOutLo = MODE == kMedian ? kMedLo : BX;
-  constexpr int kOutHi = MODE == kMedian ? kMedHi + 1 : NX - BX;
-  for (; t < ntiles; t += step) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    float v[P2];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) v[i] = buf[i * kWave + lane];
-    // every lane's reads have returned before the DMA may overwrite the tile
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + step < ntiles) dma_tile<NX>(X, t + step, step4, lane_off, lds_base);
-
-    float m = v[0];
-#pragma unroll
-    for (int i = 1; i < NX; ++i) m = __builtin_elementwise_maximum(m, v[i]);
-    int nan_cnt = 0;
-    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        const bool isn = __builtin_isnan(v[i]);
-        nan_cnt += isn ? 1 : 0;
-        v[i] = isn ? __builtin_inff() : v[i];
-      }
-    }
-    network_fast<P2, NX, kOutLo, kOutHi>(v);
-    float res;
-    if constexpr (MODE == kMedian) {
-      res = (NX & 1) ? v[kMedLo] : (v[kMedLo] + v[kMedHi]) * 0.5f;
-      if (nan_cnt > 0) res = qnan();
-    } else {
-      float acc = 0.f;
-#pragma unroll
-      for (int p = BX; p < NX - BX; ++p) acc += v[p];
-      res = acc / static_cast<float>(NX - 2 * BX);
-      if (nan_cnt > BX) res = qnan();
-    }
-    out[t * kWave + lane] = res;
-  }
-}
-
-// Two-waves-per-SIMD variant (one 512-thread workgroup per CU): rows [0, H) of
-// the next tile arrive by LDS-DMA into a 16 KiB per-wave buffer, rows [H, NX)
-// by plain loads into VGPRs (pf); both are issued right after the current
-// tile was read, so the fetch overlaps the network and two waves share each
-// SIMD's VALU issue (one wave alone issues a VALU op every 4 cycles, the
-// SIMD-32 can take one every 2).
-template <int MODE, int NX, int BX>
-__global__ void __launch_bounds__(512) select_dma2_kernel(const float* __restrict__ X, int64_t ntiles, int64_t ldx,
-                                                         float* __restrict__ out) {
-  static_assert(NX <= 128, "exact-N DMA path");
-  constexpr int H = (NX / 2) & ~3;   // rows fetched by LDS-DMA (4 per instruction)
-  constexpr int R = NX - H;          // rows prefetched into VGPRs
-  extern __shared__ __attribute__((aligned(16))) float lds_tiles2[];
-  constexpr int P = ((NX + 15) / 16) * 16;
-  constexpr int P2 = next_pow2(P);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const unsigned lane = threadIdx.x & 63u;
-  float* buf = lds_tiles2 + wave * (H * kWave);
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)buf);
-  const int64_t ldb = ldx * 4;
-  const uint64_t step4 = static_cast<uint64_t>(ldb) * 4;
-  const unsigned lane_off = static_cast<unsigned>((lane >> 4) * ldb) + (lane & 15u) * 16u;
-  const unsigned col_off = lane * 4u;
-  const int64_t step = static_cast<int64_t>(gridDim.x) * 8;
-  int64_t t = static_cast<int64_t>(blockIdx.x) * 8 + wave;
-  if (t >= ntiles) return;
-  float pf[R];
-  auto prefetch = [&](int64_t tt) {
-    dma_tile<H>(X, tt, step4, lane_off, lds_base);
-    // running SGPR row pointer (opaque: no R hoisted 64-bit row offsets)
-    const uint64_t a = reinterpret_cast<uint64_t>(X + tt * kWave + H * ldx);
-    const uint32_t alo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));        // (int -> uint32: no
-    const uint32_t ahi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));  //  sign extension)
-    uint64_t rp = (static_cast<uint64_t>(ahi) << 32) | alo;
-    typedef const __attribute__((address_space(1))) float gfloat;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      pf[i] = __builtin_nontemporal_load(reinterpret_cast<gfloat*>(rp + col_off));
-      rp += static_cast<uint64_t>(ldb);
-      opaque_sgpr(rp);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  prefetch(t);
-
-  constexpr int kMedLo = (NX - 1) / 2;
-  constexpr int kMedHi = NX / 2;
-  constexpr int kOutLo = MODE == kMedian ? kMedLo : BX;
-  constexpr int kOutHi = MODE == kMedian ? kMedHi + 1 : NX - BX;
-  for (; t < ntiles; t += step) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    float v[P2];
-#pragma unroll
-    for (int i = 0; i < H; ++i) v[i] = buf[i * kWave + lane];
-#pragma unroll
-    for (int i = 0; i < R; ++i) v[H + i] = pf[i];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + step < ntiles) prefetch(t + step);
-
-    float m = v[0];
-#pragma unroll
-    for (int i = 1; i < NX; ++i) m = __builtin_elementwise_maximum(m, v[i]);
-    int nan_cnt = 0;
-    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        const bool isn = __builtin_isnan(v[i]);
-        nan_cnt += isn ? 1 : 0;
-        v[i] = isn ? __builtin_inff() : v[i];
-      }
-    }
-    network_fast<P2, NX, kOutLo, kOutHi>(v);
-    float res;
-    if constexpr (MODE == kMedian) {
-      res = (NX & 1) ? v[kMedLo] : (v[kMedLo] + v[kMedHi]) * 0.5f;
-      if (nan_cnt > 0) res = qnan();
-    } else {
-      float acc = 0.f;
-#pragma unroll
-      for (int p = BX; p < NX - BX; ++p) acc += v[p];
-      res = acc / static_cast<float>(NX - 2 * BX);
-      if (nan_cnt > BX) res = qnan();
-    }
-    out[t * kWave + lane] = res;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// two-lane path: lanes 2c and 2c+1 share coordinate c of the wave's 32; lane h
-// holds rows h, h+2, h+4, ... (H values, P = 2H slots, n in (P/2, P]).
-//  1. NaNs are counted (only if the wave saw one) and mapped to +inf, so the
-//     compare-exchanges are plain v_min/v_max; pads are +inf (median: split
-//     -inf / +inf so the middle lands on fixed slots H-1, H).
-//  2. each lane sorts its H values (odd-even merge network);
-//  3. one cross-lane bitonic step through DPP (quad_perm [1,0,3,2]): the even
-//     lane keeps min(a_i, b_{H-1-i}), the odd lane max(b_i, a_{H-1-i}) -- both
-//     bitonic -- and both lanes finish with the same half-cleaner cascade, so
-//     the even lane ends with merged slots 0..H-1 and the odd lane H..2H-1;
-//  4. trimmed mean: the even lane sums its kept slots in ascending order, hands
-//     the partial to the odd lane (DPP), which continues -- the sequential
-//     ascending-order fp32 sum of numpy, bit for bit.
-// Half the registers of the one-lane path -> ~2x the waves in flight.
-// Requires ldx*4 < 2^31 (the odd lane's row offset is a 32-bit lane offset).
-// ---------------------------------------------------------------------------
-template <int H, int MODE, int NX, int BX, int BS = 256>
-__global__ void __launch_bounds__(BS) select2_kernel(const float* __restrict__ X, int n_rt, int64_t d,
-                                                     int64_t ldx, int lo_rt, int hi_rt, float* __restrict__ out) {
-  constexpr int P = 2 * H;
-  constexpr bool kExactN = NX > 0;
-  constexpr bool kExactB = kExactN && BX >= 0;
-  const int n = kExactN ? NX : n_rt;
-  const int lo = kExactB ? BX : lo_rt;
-  const int hi = kExactB ? NX - BX : hi_rt;
-  const unsigned h = threadIdx.x & 1u;
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * (BS / 2);
-  const int64_t rem = d - base;
-  const unsigned jl0 = threadIdx.x >> 1;
-  const unsigned last = rem < BS / 2 ? static_cast<unsigned>(rem - 1) : static_cast<unsigned>(BS / 2 - 1);
-  const unsigned jl = jl0 < last ? jl0 : last;
-  const int64_t ldb = ldx * 4;
-  const unsigned off_pair = static_cast<unsigned>(h * ldb) + jl * 4u;  // row 2i+h
-  const unsigned off_even = jl * 4u;                                     // row 2i (clamped rows)
-  const char* xb = reinterpret_cast<const char*>(X + base);
-  const int k_bottom = (MODE == kMedian) ? (P - n) / 2 : 0;
-
-  float v[H];
-  float m = 0.f;
-#pragma unroll
-  for (int i = 0; i < H; ++i) {
-    const int r0 = 2 * i;
-    float x;
-    if (r0 + 1 < n) {                       // both rows of the pair are real
-      x = ldrow(xb + r0 * ldb, off_pair);
-    } else {                                // tail: clamp to a real row, pad later
-      const int rc = r0 < n ? r0 : n - 1;
-      x = ldrow(xb + rc * ldb, off_even);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const int row = r0 + static_cast<int>(h);
-    const bool real = row < n;
-    m = (i == 0) ? x : (real ? __builtin_elementwise_maximum(m, x) : m);
-    const float pad = (row - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
-    v[i] = real ? x : pad;
-  }
-  // NaN bookkeeping (rare; wave-uniform branch)
-  int nan_cnt = 0;
-  const bool lane_nan = __builtin_isnan(m);
-  if (__builtin_amdgcn_ballot_w64(lane_nan) != 0) {
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      nan_cnt += __builtin_isnan(v[i]) ? 1 : 0;
-      v[i] = __builtin_fminf(v[i], __builtin_inff());  // NaN -> +inf
-    }
-  }
-  nan_cnt += __builtin_bit_cast(int, swap_adjacent(__builtin_bit_cast(float, nan_cnt)));
-
-  network_plain<H, H, 0, H, kNetSort>(v);
-  float w[H];
-#pragma unroll
-  for (int i = 0; i < H / 2; ++i) {
-    const int k = H - 1 - i;
-    const float pi = swap_adjacent(v[k]);
-    const float pk = swap_adjacent(v[i]);
-    w[i] = h ? __builtin_fmaxf(v[i], pi) : __builtin_fminf(v[i], pi);
-    w[k] = h ? __builtin_fmaxf(v[k], pk) : __builtin_fminf(v[k], pk);
-  }
-  network_plain<H, H, 0, H, kNetMerge>(w);
-
-  float res;
-  bool writer;
-  if constexpr (MODE == kMedian) {
-    const float t = h ? w[0] : w[H - 1];
-    const float other = swap_adjacent(t);
-    res = (n & 1) ? t : (t + other) * 0.5f;
-    if (nan_cnt > 0) res = qnan();
-    writer = h == 0;
-  } else {
-    const int e_hi = hi < H ? hi : H;
-    const int o_lo = (lo > H ? lo : H) - H;
-    const int o_hi = hi - H;
-    float acc = 0.f;
-#pragma unroll
-    for (int p = 0; p < H; ++p) {
-      if (p >= lo && p < e_hi) {
-        if constexpr (!kExactB) asm volatile("");
-        acc += w[p];
-      }
-    }
-    float acc2 = swap_adjacent(acc);
-#pragma unroll
-    for (int p = 0; p < H; ++p) {
-      if (p >= o_lo && p < o_hi) {
-        if constexpr (!kExactB) asm volatile("");
-        acc2 += w[p];
-      }
-    }
-    res = acc2 / static_cast<float>(hi - lo);
-    if (nan_cnt > n - hi) res = qnan();
-    writer = h == 1;
-  }
-  if (writer && jl0 < rem) out[base + jl0] = res;
-}
-
-// ---------------------------------------------------------------------------
 // Multi-lane path for 128 < N <= 512 (the N = 512 MoM / 8-GPU config): L = 2 or
 // 4 lanes share one coordinate, 128 values each, all in registers.
 //   lane (c, h) = lane L*c + h holds rows {L*i + h} of coordinate c (per load
@@ -863,7 +552,7 @@ static int env_int(const char* name, int dflt) {
 }
 
 // Variant selection.  Defaults are the measured-fastest; the
-// SRA_SELECT (1 = one-lane, 2 = two-lane) and SRA_BS (block size) environment
+// SRA_SELECT (1 = generic one-lane network) and SRA_BS (block size) environment
 // variables exist for A/B measurements only.
 template <int MODE>
 static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, int hi, float* out,
@@ -871,66 +560,9 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
   static const int force = env_int("SRA_SELECT", 0);
   static const int bs_env = env_int("SRA_BS", 0);
   const int P = static_cast<int>(cdiv(n, 16) * 16);
-  const bool two_lane_ok = ldx * 4 < (int64_t(1) << 31);
   const bool trim128 = MODE == kTrimmed && n == 128 && lo == 12 && hi == 116;
   const bool trim100 = MODE == kTrimmed && n == 100 && lo == 10 && hi == 90;
 
-  if (force == 2 && two_lane_ok && n > 32 && n <= 256) {
-    const int bs = bs_env == 1024 ? 1024 : 256;
-#define SRA_SEL2(HH, NXX, BXX)                                                                                   \
-  do {                                                                                                           \
-    if (bs == 1024)                                                                                              \
-      hipLaunchKernelGGL((select2_kernel<HH, MODE, NXX, BXX, 1024>), dim3(cdiv(d, 512)), dim3(1024), 0, s, X, n, d, \
-                         ldx, lo, hi, out);                                                                      \
-    else                                                                                                         \
-      hipLaunchKernelGGL((select2_kernel<HH, MODE, NXX, BXX, 256>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, \
-                         ldx, lo, hi, out);                                                                      \
-    return launch_status("select2_kernel");                                                                      \
-  } while (0)
-    if (trim128) SRA_SEL2(64, 128, 12);
-    if (MODE == kMedian && n == 128) SRA_SEL2(64, 128, -1);
-    if (n <= 64) SRA_SEL2(32, 0, -1);
-    if (n <= 128) SRA_SEL2(64, 0, -1);
-    SRA_SEL2(128, 0, -1);
-#undef SRA_SEL2
-  }
-  const bool dma_ok = force != 1 && force != 2 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
-                      d >= kWave && ldx * 4 * 4 < (int64_t(1) << 32);   // 32-bit DMA lane offsets (rows 0..3)
-  // LDS-DMA persistent variants: off by default -- measured slower than the
-  // register path at N = 100 / 128, d = 1e8; SRA_DMA_WAVES=1|2
-  // selects them for A/B runs.
-  static const int dma_waves = env_int("SRA_DMA_WAVES", 0);
-  if (dma_ok && dma_waves > 0 && (trim128 || trim100 || (MODE == kMedian && (n == 128 || n == 100)))) {
-    const int64_t ntiles = d / kWave;
-#define SRA_DMA(NXX, BXX)                                                                                        \
-  do {                                                                                                           \
-    const bool one = dma_waves == 1;                                                                             \
-    auto kern = one ? select_dma_kernel<MODE, NXX, BXX> : select_dma2_kernel<MODE, NXX, BXX>;                    \
-    const int wpb = one ? 4 : 8;                                                                                 \
-    const int lds1 = 4 * NXX * kWave * static_cast<int>(sizeof(float));                                          \
-    const int lds2 = 8 * ((NXX / 2) & ~3) * kWave * static_cast<int>(sizeof(float));                            \
-    static const hipError_t attr1 = hipFuncSetAttribute(                                                         \
-        reinterpret_cast<const void*>(select_dma_kernel<MODE, NXX, BXX>),                                       \
-        hipFuncAttributeMaxDynamicSharedMemorySize, lds1);                                                       \
-    static const hipError_t attr2 = hipFuncSetAttribute(                                                         \
-        reinterpret_cast<const void*>(select_dma2_kernel<MODE, NXX, BXX>),                                      \
-        hipFuncAttributeMaxDynamicSharedMemorySize, lds2);                                                       \
-    if ((one ? attr1 : attr2) != hipSuccess) break;                                                              \
-    const int64_t grid = std::min<int64_t>(num_cus(), cdiv(ntiles, wpb));                                        \
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * wpb), one ? lds1 : lds2, s, X, ntiles, ldx, out);             \
-    int rc = launch_status("select_dma_kernel");                                                                 \
-    if (rc || d % kWave == 0) return rc;                                                                         \
-    return launch_select<MODE>(X + ntiles * kWave, n, d - ntiles * kWave, ldx, lo, hi, out + ntiles * kWave, s); \
-  } while (0)
-    if constexpr (MODE == kTrimmed) {
-      if (trim128) SRA_DMA(128, 12);
-      if (trim100) SRA_DMA(100, 10);
-    } else {
-      if (n == 128) SRA_DMA(128, -1);
-      if (n == 100) SRA_DMA(100, -1);
-    }
-#undef SRA_DMA
-  }
   // Exact-N trimmed mean: the VOP2 min/max network with a NaN pre-pass
   // (measured 1.5-2 % faster than the VOP3 NaN-propagating one at N = 128,
   // d = 1e8; SRA_NET=0 selects the latter).  The median keeps the
@@ -980,7 +612,7 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
   }
   // 128 < N <= 512: 2 or 4 lanes per coordinate, register-resident, DPP merges
   const bool quad_ok = ldx * 4 * 3 + 256 < (int64_t(1) << 32);   // 32-bit lane offsets
-  if (quad_ok && force != 2 && n > 128 && n <= 256) {
+  if (quad_ok && n > 128 && n <= 256) {
     hipLaunchKernelGGL((select_quad_kernel<2, MODE>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, ldx, lo, hi, out);
     return launch_status("select_quad_kernel");
   }
@@ -993,11 +625,6 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
                          out);
     }
     return launch_status("select_quad_kernel");
-  }
-  if (two_lane_ok && n > 128 && n <= 256) {
-    hipLaunchKernelGGL((select2_kernel<128, MODE, 0, -1, 256>), dim3(cdiv(d, 128)), dim3(256), 0, s, X, n, d, ldx,
-                       lo, hi, out);
-    return launch_status("select2_kernel");
   }
   const int pn = next_pow2(n);
   SRA_REQUIRE(pn <= kLdsFloats / 4, SRA_ERR_UNSUPPORTED, "k-select supports N <= %d (got %d)", kLdsFloats / 4, n);

@@ -385,13 +385,14 @@ static_assert(2 * kSolveLds <= 163840, "two solver workgroups must fit one CU's 
 // principal minors, rescaled every 4 steps; the previous check's Ritz value
 // theta_lb is a lower bound by interlacing, so the first round's points are
 // geometric above it), then the eigenvector from a twisted factorisation of
-// T - lambda I (lane 0 runs the forward pivots, lane 1 the backward ones, the
-// twist is the smallest |gamma|).  The normalised eigenvector goes to
+// T - lambda I (forward and backward pivots in one wave-uniform loop held in
+// registers, the twist is the smallest |gamma|).  The normalised eigenvector goes to
 // trw[128, 128 + m); returns lambda and its last component.  Kept out of line:
 // it runs a few times per filter iteration and its registers would otherwise
 // compete with the 64 Gram values per lane of the solver's hot loop.
 __device__ __attribute__((noinline)) void tri_top(double* trw, int m, double tscale, double theta_lb, double* lam_out,
                                                   double* zlast_out) {
+  m = __builtin_amdgcn_readfirstlane(m);   // wave-uniform: scalar loop control
   const int lane = threadIdx.x & 63;
   const double al = lane < m ? trw[lane] : 0.0;
   const double b2l = lane + 1 < m ? trw[64 + lane] : 0.0;
@@ -404,60 +405,81 @@ __device__ __attribute__((noinline)) void tri_top(double* trw, int m, double tsc
   // leading principal minors, rescaled by powers of two every 4
   // steps; the previous check's Ritz value is a lower bound
   // (interlacing), so the first round's points are geometric above it
+  // T_00 = alpha_0 is a lower bound too (the start vector's Rayleigh quotient;
+  // after a restart, the previous Ritz value)
+  theta_lb = fmax(theta_lb, readlane_f64(al, 0));
   const bool geo = theta_lb > lo && theta_lb < hi;
   if (geo) lo = theta_lb;
+  constexpr double kInv65 = 1.0 / 65.0;
   for (int round = 0; round < 16; ++round) {
-    const double fr = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, lane - 63) : (lane + 1) / 65.0;
+    const double fr = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, lane - 63) : (lane + 1) * kInv65;
     const double x = lo + (hi - lo) * fr;
     double p2 = 1.0;
     double p1 = readlane_f64(al, 0) - x;
     int cntb = __builtin_signbit(p1) ? 1 : 0;
-#pragma unroll 4
-    for (int q = 1; q < m; ++q) {
-      // alpha / beta^2 broadcast from registers (readlane), off the FMA chain
+    // one step: only the fma depends on the previous step (beta^2 * p2 uses
+    // the value of two steps back); alpha / beta^2 broadcast from registers
+    auto step = [&](int q) __attribute__((always_inline)) {
       const double pk = fma(readlane_f64(al, q) - x, p1, -(readlane_f64(b2l, q - 1) * p2));
       cntb += (__builtin_signbit(pk) ? 1 : 0) != (__builtin_signbit(p1) ? 1 : 0);
       p2 = p1;
       p1 = pk;
-      if ((q & 3) == 3) {
-        const int e = __builtin_amdgcn_frexp_exp(p1);
-        p1 = __builtin_amdgcn_ldexp(p1, -e);
-        p2 = __builtin_amdgcn_ldexp(p2, -e);
-      }
+    };
+    int q = 1;
+    for (; q + 4 <= m; q += 4) {   // unrolled by hand: the rescale runs once per 4 steps
+      step(q);
+      step(q + 1);
+      step(q + 2);
+      step(q + 3);
+      const int e = __builtin_amdgcn_frexp_exp(p1);
+      p1 = __builtin_amdgcn_ldexp(p1, -e);
+      p2 = __builtin_amdgcn_ldexp(p2, -e);
     }
+    for (; q < m; ++q) step(q);
     const unsigned long long ok = __builtin_amdgcn_ballot_w64(cntb >= m);
     const int first = ok ? __builtin_ctzll(ok) : 64;
     const double flo = first == 0 ? 0.0
                                   : ((geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 64)
-                                                         : first / 65.0);
-    const double fhi = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 63) : (first + 1) / 65.0;
+                                                         : first * kInv65);
+    const double fhi = (geo && round == 0) ? __builtin_amdgcn_ldexp(1.0, first - 63) : (first + 1) * kInv65;
     const double nlo = lo + (hi - lo) * flo;
     const double nhi = first < 64 ? lo + (hi - lo) * fhi : hi;
+    const bool stalled = nlo == lo && nhi == hi;   // a bracket of a few ulps no longer splits
     lo = nlo;
     hi = nhi;
-    if (hi - lo <= 2e-16 * fmax(fabs(lo), fabs(hi))) break;
+    // two ulps: one ulp is up to 2.2e-16 relative, so a 2e-16 test could
+    // never pass just above a power of two and every check ran all 16 rounds
+    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
   }
   const double lm = 0.5 * (lo + hi);
-  // eigenvector of T - lm I by a twisted factorisation: lane 0 runs the
-  // forward pivots dp (into s), lane 1 the backward pivots dm (into the
-  // scratch) in one serial loop; the twist is the smallest |gamma|
+  // eigenvector of T - lm I by a twisted factorisation.  The forward pivots
+  // dp_q (q = k) and the backward pivots dm_q (q = m - 1 - k) run in one
+  // wave-uniform serial loop on alpha / beta^2 broadcast from registers; lane
+  // q keeps dp_q and dm_q (no LDS round trip on the chain); the twist is the
+  // smallest |gamma|
   const double tiny = 1e-300 + 1e-30 * tscale;
-  if (lane < 2) {
-    const bool fw = lane == 0;
-    double piv = 0.0;
+  double dpl = 0.0, dml = 0.0;
+  {
+    double pf = 0.0, pb = 0.0;
     for (int k = 0; k < m; ++k) {
-      const int q = fw ? k : m - 1 - k;
-      double v = trw[q] - lm;
-      if (k > 0) v -= fdiv(trw[64 + (fw ? q - 1 : q)], piv);
-      if (fabs(v) < tiny) v = -tiny;
-      piv = v;
-      trw[(fw ? 128 : 192) + q] = v;
+      const int qf = k, qb = m - 1 - k;
+      double vf = readlane_f64(al, qf) - lm;
+      double vb = readlane_f64(al, qb) - lm;
+      if (k > 0) {
+        vf -= fdiv(readlane_f64(b2l, qf - 1), pf);
+        vb -= fdiv(readlane_f64(b2l, qb), pb);
+      }
+      if (fabs(vf) < tiny) vf = -tiny;
+      if (fabs(vb) < tiny) vb = -tiny;
+      pf = vf;
+      pb = vb;
+      dpl = lane == qf ? vf : dpl;
+      dml = lane == qb ? vb : dml;
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  const double dpl = lane < m ? trw[128 + lane] : 0.0;
-  const double dml = lane < m ? trw[192 + lane] : 0.0;
-  const double dmn = lane + 1 < m ? trw[192 + lane + 1] : 1.0;
+  // the shuffle runs with every lane active (a disabled source lane reads 0)
+  const double dmx = __shfl_down(dml, 1);
+  const double dmn = lane + 1 < m ? dmx : 1.0;
   double gam = lane < m ? fabs(dpl + dml - (al - lm)) : 1e308;
   int tw = lane;
 #pragma unroll
@@ -471,30 +493,34 @@ __device__ __attribute__((noinline)) void tri_top(double* trw, int m, double tsc
   }
   tw = __builtin_amdgcn_readfirstlane(tw);
   // z_tw = 1; z_q = -(b_q / dp_q) z_{q+1} below the twist,
-  // z_{q+1} = -(b_q / dm_{q+1}) z_q above it: ratios per lane, then
-  // lane 0 walks down and lane 1 up (into s)
+  // z_{q+1} = -(b_q / dm_{q+1}) z_q above it: ratios per lane, then both
+  // walks in one wave-uniform loop (lane q keeps z_q)
   const double rat = lane < tw ? -bl / dpl : (lane + 1 < m ? -bl / dmn : 0.0);
-  __builtin_amdgcn_wave_barrier();
-  if (lane < m) trw[192 + lane] = rat;
-  __builtin_amdgcn_wave_barrier();
-  if (lane < 2) {
-    const bool down = lane == 0;
-    double z = 1.0;
-    if (down) trw[128 + tw] = 1.0;
-    const int steps = down ? tw : m - 1 - tw;
+  double zv = lane == tw ? 1.0 : 0.0;
+  {
+    double zd = 1.0, zu = 1.0;
+    const int sd = tw, su = m - 1 - tw;
+    const int steps = sd > su ? sd : su;
     for (int k = 0; k < steps; ++k) {
-      const int q = down ? tw - 1 - k : tw + k;   // ratio index
-      z *= trw[192 + q];
-      if (fabs(z) > 1e150) z = copysign(1e150, z);   // z_tw = 1 is the largest in exact arithmetic
-      trw[128 + (down ? q : q + 1)] = z;
+      if (k < sd) {
+        const int q = tw - 1 - k;
+        zd *= readlane_f64(rat, q);
+        if (fabs(zd) > 1e150) zd = copysign(1e150, zd);   // z_tw = 1 is the largest in exact arithmetic
+        zv = lane == q ? zd : zv;
+      }
+      if (k < su) {
+        const int q = tw + k;
+        zu *= readlane_f64(rat, q);
+        if (fabs(zu) > 1e150) zu = copysign(1e150, zu);
+        zv = lane == q + 1 ? zu : zv;
+      }
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  double zv = lane < m ? trw[128 + lane] : 0.0;
   const double amax = wave_max(fabs(zv));
   const double zs = zv / amax;
   zv = zs / sqrt(wave_sum(zs * zs));
   if (lane < m) trw[128 + lane] = zv;
+  __builtin_amdgcn_wave_barrier();
   *lam_out = lm;
   *zlast_out = readlane_f64(zv, m - 1);
 }
@@ -717,6 +743,7 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
     double ui = 0.0;          // Ritz vector (warm start of the next iteration)
     bool have_u = false;
     int m_hint = 12;          // Lanczos steps the previous iteration needed
+    double rate_hint = 0.0;   // last measured log-decay of the Ritz residual per step (0: none yet)
 
     for (int it = 0; it < iters; ++it) {
       const long long t_it = dbg ? clock64() : 0;
@@ -779,12 +806,15 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
                 break;
               }
               if (j == LMAX) break;   // restart from the Ritz vector
-              // next check: extrapolate the residual's geometric decay
+              // next check: extrapolate the residual's geometric decay (this
+              // cycle's two last checks, else the last rate measured); a check
+              // costs about two Lanczos steps, so no cap short of the basis size
               int adv = 4;
-              if (m_a >= 0 && res_a > resid && resid > 0.0) {
-                const double rate = log(resid / res_a) / (m - m_a);
+              double rate = rate_hint;
+              if (m_a >= 0 && res_a > resid && resid > 0.0) rate = rate_hint = log(resid / res_a) / (m - m_a);
+              if (rate < 0.0 && resid > 0.0) {
                 const double need = log(kResTol * fabs(lm) / resid) / rate;
-                adv = need < 1.0 ? 1 : (need > 8.0 ? 8 : static_cast<int>(ceil(need)));
+                adv = need < 1.0 ? 1 : (need > LMAX ? LMAX : static_cast<int>(ceil(need)));
               }
               m_a = m;
               res_a = resid;

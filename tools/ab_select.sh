@@ -16,7 +16,5 @@ for cfg in "trimmedmean 128" "trimmedmean 100" "median 128"; do
   agg=$1; n=$2
   run ${agg}_n${n}_reg256 SRA_SELECT=1 SRA_BS=256 $B --agg $agg --clients $n
   run ${agg}_n${n}_reg768 SRA_SELECT=1 SRA_BS=768 $B --agg $agg --clients $n
-  run ${agg}_n${n}_two256 SRA_SELECT=2 SRA_BS=256 $B --agg $agg --clients $n
-  run ${agg}_n${n}_two1024 SRA_SELECT=2 SRA_BS=1024 $B --agg $agg --clients $n
 done
 echo "== done" | tee -a "$OUT/summary.txt"
