@@ -139,6 +139,16 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
                    int32_t* selected, void* ws, size_t ws_bytes, void* stream);
 
 
+/* The per-coordinate Bulyan stage alone on theta float32 rows (row i = the
+ * i-th selected vector in selection order, row stride lds): out[j] (float64)
+ * as sra_bulyan_f32's final stage computes it for robust_estimator.py:324-330
+ * (bulyan_one_coordinate over np_grads[:, j], beta = theta - 2f, Python slice
+ * semantics for beta < 0).  1 <= theta <= 128; workspace from
+ * sra_bulyan_stage_workspace_bytes (8 d bytes plus a few hundred). */
+int sra_bulyan_stage_workspace_bytes(int64_t theta, int64_t d, size_t* bytes);
+int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, int64_t lds, int32_t beta, double* out,
+                         void* ws, size_t ws_bytes, void* stream);
+
 /* The per-coordinate Bulyan stage on float64 values, any input order:
  * robust_estimator.bulyan_median (src/robust_estimator.py:259-270) and
  * bulyan_one_coordinate (:272-275) for every column of the theta x d matrix A

@@ -361,97 +361,170 @@ __device__ double bulyan_stage_generic(A&& a, int theta, int keep, Slot&& slot, 
   return np_pw64(0, keep, [&](int p) { return a(slot(p)); }) / static_cast<double>(keep);
 }
 
-template <int P>  // theta <= P; 64-thread blocks (one wave), sorted columns in LDS
-__global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
-                                                          const int* __restrict__ rows, int theta, int keep,
-                                                          int64_t d, double* __restrict__ out) {
+// numpy's pairwise fp64 sum (np_pw_block64) of f(0..n) for n in (P - 16, P],
+// unrolled over static indices so that f may read registers; n is wave-uniform
+template <int P, typename F>
+__device__ __forceinline__ double np_pw_static64(int n, F&& f) {
+  static_assert(P <= 128, "one pairwise block");
+  if (n < 8) {
+    double res = 0.0;
+#pragma unroll
+    for (int i = 0; i < (P < 8 ? P : 8); ++i)
+      if (i < n) res += f(i);
+    return res;
+  }
+  const int nb = n - (n % 8);
+  double r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = f(k);
+#pragma unroll
+  for (int i = 8; i + 8 <= P; i += 8)
+    if (i < nb) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] += f(i + k);
+    }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+  for (int i = (P > 16 ? P - 16 : 8); i < P; ++i)
+    if (i >= nb && i < n) res += f(i);
+  return res;
+}
+
+// The mean of the keep values nearest the centre c = s(p0) of a sorted column
+// (s(p), p < theta), for a column whose partial sums are all exact in fp64:
+// the order of summation is then immaterial, and the window is
+// [pl - a, pr + k - a] around the run [pl, pr] of values equal to c, with a
+// found by bisection (left element i is taken iff the (k - i + 1)-th right
+// element is not strictly nearer: robust_estimator.py:272-275 takes the run
+// first, then grows left on <= ties).
+template <typename Col>
+__device__ double bulyan_window_mean(Col&& s, int theta, int keep, int p0) {
+  const double c = s(p0);
+  int pl = p0, pr = p0;
+  while (pl > 0 && static_cast<double>(s(pl - 1)) == c) --pl;
+  while (pr + 1 < theta && static_cast<double>(s(pr + 1)) == c) ++pr;
+  const int run = pr - pl + 1;
+  if (keep <= run) return c;   // keep copies of c
+  const int k = keep - run, nl = pl, nr = theta - 1 - pr;
+  int lo = k - nr > 0 ? k - nr : 0, hi = k < nl ? k : nl;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    const int jr = k - mid + 1;
+    const bool taken = jr > nr || static_cast<double>(s(pr + jr)) - c >= c - static_cast<double>(s(pl - mid));
+    if (taken) lo = mid;
+    else hi = mid - 1;
+  }
+  double acc = static_cast<double>(run) * c;
+  for (int p = pl - lo; p < pl; ++p) acc += static_cast<double>(s(p));
+  for (int p = pr + 1; p <= pr + k - lo; ++p) acc += static_cast<double>(s(p));
+  return acc / static_cast<double>(keep);
+}
+
+constexpr int kFinalMaxTheta = 128;
+
+// value v[i] of a register array at a wave-uniform runtime index i in
+// [(P - 16) / 2 - 1, P / 2] (theta in (P - 16, P]): a select chain; the empty
+// asm keeps the optimiser from folding it back into an indexed (scratch) load
+template <int P, int P2>
+__device__ __forceinline__ float pick_hi(const float (&v)[P2], int i) {   // i in [P - 16, P)
+  float r = v[P - 1];
+#pragma unroll
+  for (int q = (P > 16 ? P - 16 : 0); q < P - 1; ++q) {
+    r = i == q ? v[q] : r;
+    asm volatile("" : "+v"(r));
+  }
+  return r;
+}
+template <int P, int P2>
+__device__ __forceinline__ float pick_mid(const float (&v)[P2], int i) {
+  constexpr int lo = (P > 16 ? (P - 16) / 2 - 1 : 0);
+  float r = v[P / 2];
+#pragma unroll
+  for (int q = lo; q < P / 2; ++q) {
+    r = i == q ? v[q] : r;
+    asm volatile("" : "+v"(r));
+  }
+  return r;
+}
+
+// Columns the final kernel lists, entry = 2 j + kind:
+//   kind 1 -- a NaN or an infinity among the values: the per-coordinate stage
+//             by definition (bulyan_stage_generic), LDS rank scratch;
+//   kind 0 -- finite, but the magnitude span lets fp64 rounding decide: the
+//             centre from numpy's pairwise totals of the two middle values
+//             (first index on a tie), then the window walked in argsort order
+//             (run first, grow left on <= ties) and summed with numpy's
+//             eight-accumulator scheme, as robust_estimator.py:259-275 does.
+// One lane per listed column, any number of columns per lane (the count is
+// only known on the device); a few per million columns in practice.
+template <int P>
+__global__ void __launch_bounds__(64) bulyan_listed_kernel(const float* __restrict__ S, int64_t lds_,
+                                                           const int* __restrict__ rows, int theta, int keep,
+                                                           const int* __restrict__ nf_count,
+                                                           const int64_t* __restrict__ nf_list,
+                                                           double* __restrict__ out) {
   constexpr int P2 = next_pow2(P);
   __shared__ float col[P][64];
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * 64;
-  const int64_t rem = d - base;
   const int t = threadIdx.x;
-  const int tl = t < rem ? t : static_cast<int>(rem - 1);
-  const int64_t j = base + tl;
-  auto a_orig = [&](int i) -> float { return S[static_cast<int64_t>(rows[i]) * lds_ + j]; };
-
-  float v[P2];
-  bool nonfinite = false;
+  const int cnt = *nf_count;
+  for (int e = blockIdx.x * 64 + t; e < cnt; e += gridDim.x * 64) {
+    const int64_t j = nf_list[e] >> 1;
+    auto a = [&](int i) -> float { return S[static_cast<int64_t>(rows[i]) * lds_ + j]; };
+    if (nf_list[e] & 1) {
+      int m;
+      out[j] = keep == 0 ? __builtin_nan("")
+                         : bulyan_stage_generic([&](int i) -> double { return a(i); }, theta, keep,
+                                                [&](int p) -> int& { return *reinterpret_cast<int*>(&col[p][t]); },
+                                                &m);
+      continue;
+    }
+    if (keep == 0) {
+      out[j] = __builtin_nan("");
+      continue;
+    }
+    float o[P2], v[P2];
 #pragma unroll
-  for (int i = 0; i < P; ++i) {
-    const float x = i < theta ? a_orig(i) : __builtin_inff();
-    nonfinite |= i < theta && !__builtin_isfinite(x);
-    v[i] = x;
-  }
-  if (__builtin_amdgcn_ballot_w64(nonfinite) != 0) {
+    for (int i = 0; i < P; ++i) {
+      o[i] = i < theta ? a(i) : __builtin_inff();
+      v[i] = o[i];
+    }
+    network_fast<P2, P, 0, P>(v);
 #pragma unroll
-    for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
-  }
-  network_fast<P2, P, 0, P>(v);
-#pragma unroll
-  for (int i = 0; i < P; ++i) col[i][t] = v[i];
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  if (nonfinite) {
-    // a NaN or an infinity changes which value is the centre (see
-    // bulyan_stage_generic); this lane's own LDS column is its scratch
-    int m;
-    const double r = bulyan_stage_generic([&](int i) -> double { return a_orig(i); }, theta, keep,
-                                          [&](int p) -> int& { return *reinterpret_cast<int*>(&col[p][t]); }, &m);
-    if (t < rem) out[base + t] = r;
-    return;
-  }
-  const int live = theta;
-
-  // 1. Bulyan median
-  double am;
-  if (theta & 1) {
-    am = col[(theta - 1) / 2][t];
-  } else {
-    // middle order statistics, fp64 pairwise tie-break
-    const float L = col[theta / 2 - 1][t];
-    const float U = col[theta / 2][t];
-    if (L == U) {
-      am = L;
+    for (int i = 0; i < P; ++i) col[i][t] = v[i];
+    double am;
+    if (theta & 1) {
+      am = col[(theta - 1) / 2][t];
     } else {
-      const double TL = np_pw64(0, theta, [&](int i) { return __builtin_fabs(static_cast<double>(L) - a_orig(i)); });
-      const double TU = np_pw64(0, theta, [&](int i) { return __builtin_fabs(static_cast<double>(U) - a_orig(i)); });
-      if (TL < TU) {
+      const float L = col[theta / 2 - 1][t], U = col[theta / 2][t];
+      if (L == U) {
         am = L;
-      } else if (TU < TL) {
-        am = U;
       } else {
-        int fL = theta, fU = theta;
-        for (int i = theta - 1; i >= 0; --i) {
-          const float a = a_orig(i);
-          if (a == L) fL = i;
-          if (a == U) fU = i;
+        const double TL = np_pw_static64<P>(theta, [&](int i) { return __builtin_fabs(static_cast<double>(L) - o[i]); });
+        const double TU = np_pw_static64<P>(theta, [&](int i) { return __builtin_fabs(static_cast<double>(U) - o[i]); });
+        int fl = theta, fu = theta;
+#pragma unroll
+        for (int i = P - 1; i >= 0; --i) {
+          fl = o[i] == L ? i : fl;
+          fu = o[i] == U ? i : fu;
         }
-        am = fL < fU ? L : U;
+        am = (TL < TU || (TL == TU && fl < fu)) ? L : U;
       }
     }
-  }
-  double res;
-  if (keep == 0) {
-    res = __builtin_nan("");   // mean of an empty slice
-  } else {
-    // 2. run of values equal to a_m in the sorted column (a_m is one of them)
-    int pl = (live - 1) / 2, pr;
+    // run of values equal to am in the sorted column, then the walk
+    int pl = (theta - 1) / 2;
     while (pl > 0 && static_cast<double>(col[pl][t]) > am) --pl;
-    while (pl < live - 1 && static_cast<double>(col[pl][t]) < am) ++pl;
+    while (pl < theta - 1 && static_cast<double>(col[pl][t]) < am) ++pl;
     while (pl > 0 && static_cast<double>(col[pl - 1][t]) == am) --pl;
-    pr = pl;
-    while (pr + 1 < live && static_cast<double>(col[pr + 1][t]) == am) ++pr;
-
-    // 3. the keep nearest, in argsort (distance) order; 4. numpy pairwise fp64 mean
+    int pr = pl;
+    while (pr + 1 < theta && static_cast<double>(col[pr + 1][t]) == am) ++pr;
     int l = pl, r = pr, taken = 0;
     auto next = [&]() -> double {
-      // run elements first (distance 0), then grow left on <= ties
       if (taken < pr - pl + 1) {
         ++taken;
         return am;
       }
       const double dl = l > 0 ? am - static_cast<double>(col[l - 1][t]) : __builtin_inf();
-      const double dr = r < live - 1 ? static_cast<double>(col[r + 1][t]) - am : __builtin_inf();
+      const double dr = r < theta - 1 ? static_cast<double>(col[r + 1][t]) - am : __builtin_inf();
       ++taken;
       if (dl <= dr) {
         --l;
@@ -460,12 +533,11 @@ __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restric
       ++r;
       return static_cast<double>(col[r][t]);
     };
+    double res;
     if (keep < 8) {
       res = 0.0;
       for (int i = 0; i < keep; ++i) res += next();
     } else {
-      // eight accumulators over the first keep - keep%8 values, then the tail
-      // (keep <= theta <= 128)
       double r0 = next(), r1 = next(), r2 = next(), r3 = next(), r4 = next(), r5 = next(), r6 = next(), r7 = next();
       int i = 8;
       for (; i < keep - (keep % 8); i += 8) {
@@ -475,9 +547,159 @@ __global__ void __launch_bounds__(64) bulyan_final_kernel(const float* __restric
       res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
       for (; i < keep; ++i) res += next();
     }
-    res = res / static_cast<double>(keep);
+    out[j] = res / static_cast<double>(keep);
   }
-  if (t < rem) out[base + t] = res;
+}
+
+// Four waves per block, one lane per coordinate.  The theta selected values
+// are gathered in selection order (row indices broadcast from VGPRs by
+// readlane) and sorted in registers.  The sorted column goes through ONE LDS
+// tile per block that the four waves take in turn (a barrier per turn), so
+// LDS does not cap the occupancy (round 1's per-wave tile allowed 6 waves per
+// CU: 5.3 ms at theta = 88, d = 1e7).  In its turn a wave checks the column's
+// magnitude span -- when every partial sum of values and of |differences| is
+// exact in fp64 the result does not depend on summation order -- and finds
+// the windows of the centre candidates by bisection.  The even-theta
+// tie-break between the two middle values re-reads the column in selection
+// order: their totals are then equal, so the first index holding either
+// value decides, as np.argmin does.  Columns failing the span test, or
+// holding a NaN or an infinity, go to bulyan_listed_kernel.
+template <int P>  // theta in (P - 16, P]
+__global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
+                                                           const int* __restrict__ rows, int theta, int keep,
+                                                           int64_t d, double* __restrict__ out,
+                                                           int* __restrict__ nf_count, int64_t* __restrict__ nf_list) {
+  constexpr int P2 = next_pow2(P);
+  __shared__ float col[P][64];
+  const int t = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 + wave * 64;
+  const int64_t rem = d - base;   // may be <= 0 for the last block's trailing waves
+  const int tl = rem <= 0 ? 0 : (t < rem ? t : static_cast<int>(rem - 1));
+  const int64_t j = rem <= 0 ? d - 1 : base + tl;
+  constexpr int RW = (P + 63) / 64;
+  int rl[RW];
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int li = 64 * q + t;
+    rl[q] = rows[li < theta ? li : theta - 1];
+  }
+  const int64_t jb = j - tl;   // this wave's first coordinate (clamped)
+  const unsigned off = static_cast<unsigned>(tl) * 4u;
+  constexpr int kFirstPad = P > 16 ? P - 16 : 0;
+  auto load_col = [&](float (&v)[P2], bool& nonfinite) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int row = __builtin_amdgcn_readlane(rl[i / 64], i % 64);
+      const char* rp = uniform_ptr(reinterpret_cast<const char*>(S + static_cast<int64_t>(row) * lds_ + jb));
+      const float x = ld_lane(rp, off);
+      // one row address at a time in SGPRs (hoisting all of them spills)
+      __builtin_amdgcn_sched_barrier(0);
+      // rows below P - 16 always exist (theta > P - 16): no per-row predicate
+      const bool real = i < kFirstPad || i < theta;
+      v[i] = real ? x : __builtin_inff();
+      nonfinite |= real && !__builtin_isfinite(x);
+    }
+  };
+
+  const bool even = (theta & 1) == 0;
+  float cl, cu;            // centre candidates: the two middle values (even theta) or the median (cl)
+  bool nonfinite = false;
+  {
+    float v[P2];
+    load_col(v, nonfinite);
+    if (__builtin_amdgcn_ballot_w64(nonfinite) != 0) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
+    }
+    network_fast<P2, P, 0, P>(v);
+    cl = pick_mid<P, P2>(v, even ? theta / 2 - 1 : (theta - 1) / 2);
+    cu = pick_mid<P, P2>(v, theta / 2);
+    // magnitude span: every value, |x - y| and partial sum of <= 128 of them
+    // is a multiple of ulp(smallest nonzero |value|) below 256 max|value|;
+    // exact in fp64 when that spans <= 53 bits.  |value| bits compare as
+    // unsigned integers; the +inf padding never wins the minimum, and the
+    // maximum magnitude is at one end of the sorted column.
+    bool exact = true;   // all sums exact in fp64
+    {
+      unsigned mnb = 0xffffffffu;   // (smallest nonzero |value| bits) - 1
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const unsigned ab = (__builtin_bit_cast(unsigned, v[i]) & 0x7fffffffu) - 1u;   // 0 wraps: ignored
+        mnb = ab < mnb ? ab : mnb;
+      }
+      const unsigned mxb = fmaxf(-v[0], pick_hi<P, P2>(v, theta - 1)) < 0.f
+                               ? 0u : __builtin_bit_cast(unsigned, fmaxf(-v[0], pick_hi<P, P2>(v, theta - 1)));
+      if (mnb != 0xffffffffu) {
+        const int emx = static_cast<int>(mxb >> 23) - 126;   // max|x| < 2^emx
+        const int ebn = static_cast<int>((mnb + 1u) >> 23);
+        const int ulp = (ebn > 0 ? ebn : 1) - 150;          // ulp(min nonzero |x|) = 2^ulp
+        exact = (emx + 8) - ulp <= 53;
+      }
+    }
+    // this wave's turn with the LDS tile: wave w works between the block's
+    // barriers w + 1 and w + 2 (every wave passes four), so the sorted values
+    // are dead once stored and do not share registers with the window search
+    double res_l = 0.0, res_u = 0.0;
+#pragma unroll 1
+    for (int w = 0; w <= wave; ++w) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < P; ++i) col[i][t] = v[i];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    auto s = [&](int p) -> float { return col[p][t]; };
+    if (keep == 0) {
+      // the mean of an empty slice: NaN for every column, written below
+    } else if (nonfinite) {
+      // a NaN or an infinity changes which value is the centre (see
+      // bulyan_stage_generic): listed for bulyan_listed_kernel
+      if (rem > 0 && t < rem) nf_list[atomicAdd(nf_count, 1)] = 2 * j + 1;
+    } else {
+      if (exact) {
+        res_l = bulyan_window_mean(s, theta, keep, even ? theta / 2 - 1 : (theta - 1) / 2);
+        if (even && cu != cl) res_u = bulyan_window_mean(s, theta, keep, theta / 2);
+      } else if (rem > 0 && t < rem) {
+        // rounding decides the centre and the order of the sums
+        nf_list[atomicAdd(nf_count, 1)] = 2 * j;
+      }
+    }
+#pragma unroll 1
+    for (int w = wave + 1; w < 4; ++w) __syncthreads();
+    // no early return from here on: the tie-break's gather broadcasts row
+    // indices across lanes (readlane), which must not read the register
+    // slots of lanes that left (the compiler may have copied the row list
+    // under a partial exec mask, leaving stale values there)
+    bool write = rem > 0 && t < rem && (keep == 0 || (!nonfinite && exact));   // else listed for bulyan_listed_kernel
+    double result = res_l;
+    bool tie = false;
+    if (keep == 0) result = __builtin_nan("");   // mean of an empty slice
+    else if (even && cu != cl) tie = true;
+    if (__builtin_amdgcn_ballot_w64(write && tie) != 0) {   // wave-uniform: every lane active
+      // even theta, two distinct middle values: np.argmin over the totals.
+      // The row list is reloaded here, with every lane active, and kept opaque
+      // (the first gather's row addresses are then not held live for reuse)
+#pragma unroll
+      for (int q = 0; q < RW; ++q) {
+        const int li = 64 * q + t;
+        rl[q] = rows[li < theta ? li : theta - 1];
+        asm volatile("" : "+v"(rl[q]));
+      }
+      float o[P2];
+      bool dummy = false;
+      load_col(o, dummy);
+      int fl = theta, fu = theta;
+#pragma unroll
+      for (int i = P - 1; i >= 0; --i) {
+        // padding slots hold +inf, never a (finite) centre value
+        fl = o[i] == cl ? i : fl;
+        fu = o[i] == cu ? i : fu;
+      }
+      // exact sums: the two totals are equal (the middle values split the
+      // column in halves), so np.argmin takes the first index holding either
+      if (tie) result = fl < fu ? res_l : res_u;
+    }
+    if (write) out[base + t] = result;
+  }
 }
 
 // arr[np.argsort(distances)[:beta]] keeps min(beta, theta) values for beta >= 0
@@ -513,18 +735,10 @@ __global__ void __launch_bounds__(64) bulyan_coord_f64_kernel(const double* __re
 // ---------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------
-struct BulyanWs {
-  char* krum_ws;      // krum mode
-  size_t krum_bytes;
-  int* order;         // theta selected client indices (krum) / identity rows (S)
-  int* rows_a;        // row lists (ping-pong)
-  int* rows_b;
-  int* status;
-  float* S;           // theta x d aggregates (median / trimmed modes)
-  float* partial;     // N x kDistChunks
-};
 
-size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
+// workspace: [0, 256) nonfinite-column count | order, row lists, status |
+// krum workspace or (S, partial sums) | the nonfinite-column list (int64 x d)
+static size_t bulyan_body_bytes(int n, int64_t d, int mode, int f) {
   const int theta = n - 2 * f;
   size_t b = 4096 + 4 * static_cast<size_t>(n) * 4 + 256;
   if (mode == kBulyanKrum) {
@@ -533,7 +747,11 @@ size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
     b += sizeof(float) * static_cast<size_t>(theta > 0 ? theta : 0) * static_cast<size_t>(d) + 256;
     b += sizeof(float) * static_cast<size_t>(n) * kDistChunks;
   }
-  return b;
+  return (b + 255) / 256 * 256;
+}
+
+size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
+  return bulyan_body_bytes(n, d, mode, f) + sizeof(int64_t) * static_cast<size_t>(d);
 }
 
 template <int MODE>
@@ -556,21 +774,29 @@ static int launch_select_rows(const float* X, int64_t ldx, const int* rows, int 
 }
 
 static int launch_final(const float* S, int64_t lds_, const int* rows, int theta, int beta, int64_t d, double* out,
-                        hipStream_t s) {
+                        int* nf_count, int64_t* nf_list, hipStream_t s) {
   const int keep = bulyan_keep(theta, beta);
-  const int64_t blocks = cdiv(d, 64);
+  const int64_t blocks = cdiv(d, 256);
   const int P = static_cast<int>(cdiv(theta, 16) * 16);
+  SRA_REQUIRE(theta >= 1 && theta <= kFinalMaxTheta, SRA_ERR_UNSUPPORTED,
+              "bulyan per-coordinate stage supports theta <= %d (got %d)", kFinalMaxTheta, theta);
+  SRA_HIP(hipMemsetAsync(nf_count, 0, sizeof(int), s));
+  int rc = SRA_ERR_UNSUPPORTED;
 #define SRA_FIN(PP)                                                                                              \
   case PP:                                                                                                       \
-    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(blocks), dim3(64), 0, s, S, lds_, rows, theta, keep, d, out); \
-    return launch_status("bulyan_final_kernel");
+    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(blocks), dim3(256), 0, s, S, lds_, rows, theta, keep, d, out, \
+                       nf_count, nf_list);                                                                       \
+    rc = launch_status("bulyan_final_kernel");                                                                   \
+    if (rc) return rc;                                                                                           \
+    hipLaunchKernelGGL((bulyan_listed_kernel<PP>), dim3(256), dim3(64), 0, s, S, lds_, rows, theta, keep, nf_count, \
+                       nf_list, out);                                                                            \
+    return launch_status("bulyan_listed_kernel");
   switch (P) {
     SRA_FIN(16) SRA_FIN(32) SRA_FIN(48) SRA_FIN(64) SRA_FIN(80) SRA_FIN(96) SRA_FIN(112) SRA_FIN(128)
     default: break;
   }
 #undef SRA_FIN
-  set_error("bulyan per-coordinate stage supports theta <= 128 (got %d)", theta);
-  return SRA_ERR_UNSUPPORTED;
+  return rc;
 }
 
 __global__ void iota_kernel(int* p, int n) {
@@ -596,12 +822,14 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   int* rows_b = rows_a + n;
   int* status = rows_b + n;
   char* rest = p + 4096 + 4 * static_cast<size_t>(n) * 4;
+  int* nf_count = reinterpret_cast<int*>(p);
+  int64_t* nf_list = reinterpret_cast<int64_t*>(p + bulyan_body_bytes(n, d, mode, f));
   int rc;
   if (mode == kBulyanKrum) {
     rc = launch_krum(X, n, d, ldx, dba ? f + 1 : f, theta, order, nullptr, rest, krum_workspace_bytes(n, d), s);
     if (rc) return rc;
     if (sel_out) SRA_HIP(hipMemcpyAsync(sel_out, order, sizeof(int) * theta, hipMemcpyDeviceToDevice, s));
-    return launch_final(X, ldx, order, theta, beta, d, out, s);
+    return launch_final(X, ldx, order, theta, beta, d, out, nf_count, nf_list, s);
   }
   SRA_REQUIRE(n <= 128, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= 128 (got %d)", n);
   float* S = reinterpret_cast<float*>(rest);
@@ -644,7 +872,7 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
     cur = nxt;
     nxt = tmp;
   }
-  return launch_final(S, d, order, theta, beta, d, out, s);
+  return launch_final(S, d, order, theta, beta, d, out, nf_count, nf_list, s);
 }
 
 }  // namespace sra
@@ -687,4 +915,35 @@ extern "C" int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t
   hipLaunchKernelGGL(bulyan_coord_f64_kernel, dim3(cdiv(d, 64)), dim3(64), 0, static_cast<hipStream_t>(stream), A,
                      static_cast<int>(theta), d, lda, keep, out, median_index, median_row, ldr);
   return launch_status("bulyan_coord_f64_kernel");
+}
+
+// The per-coordinate stage alone over theta float32 rows (row i = the i-th
+// selected vector, in selection order): the final stage of sra_bulyan_f32 for
+// selections made elsewhere (a d-sharded Bulyan, a caller's own rounds).
+extern "C" int sra_bulyan_stage_workspace_bytes(int64_t theta, int64_t d, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(theta >= 1 && theta <= kFinalMaxTheta && d >= 1, SRA_ERR_SHAPE, "need 1 <= theta <= %d, d >= 1",
+              kFinalMaxTheta);
+  *bytes = 256 + (static_cast<size_t>(theta) * sizeof(int) + 255) / 256 * 256 + sizeof(int64_t) * static_cast<size_t>(d);
+  return SRA_OK;
+}
+
+extern "C" int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, int64_t lds, int32_t beta, double* out,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(S != nullptr && out != nullptr && ws != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(theta >= 1 && theta <= kFinalMaxTheta, SRA_ERR_UNSUPPORTED, "1 <= theta <= %d (got %lld)",
+              kFinalMaxTheta, static_cast<long long>(theta));
+  SRA_REQUIRE(d >= 1 && lds >= d, SRA_ERR_SHAPE, "bad d / lds");
+  size_t need = 0;
+  sra_bulyan_stage_workspace_bytes(theta, d, &need);
+  SRA_REQUIRE(ws_bytes >= need, SRA_ERR_WORKSPACE, "bulyan stage workspace too small: need %zu bytes", need);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* p = static_cast<char*>(ws);
+  int* nf_count = reinterpret_cast<int*>(p);
+  int* rows = reinterpret_cast<int*>(p + 256);
+  int64_t* nf_list = reinterpret_cast<int64_t*>(p + 256 + (static_cast<size_t>(theta) * sizeof(int) + 255) / 256 * 256);
+  hipLaunchKernelGGL(iota_kernel, dim3(cdiv(theta, 256)), dim3(256), 0, s, rows, static_cast<int>(theta));
+  const int rc = launch_status("iota_kernel");
+  if (rc) return rc;
+  return launch_final(S, lds, rows, static_cast<int>(theta), beta, d, out, nf_count, nf_list, s);
 }

@@ -114,59 +114,169 @@ __device__ __forceinline__ int slice_count(int size_, int len) {
   return c > 0 ? c : 0;
 }
 
+// numpy's eight-accumulator pairwise block (n <= 128) of a[0..n) over one
+// wave: lanes 0..7 run the eight accumulators (a[k], a[k+8], ... in order),
+// then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) and the tail, every lane computing
+// the same value; n < 8 is the plain sequential sum.
+__device__ __forceinline__ float wave_pw_block_f32(const float* a, int n) {
+  const int lane = threadIdx.x & 63;
+  if (n < 8) {
+    float res = 0.f;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  const int n8 = n - (n % 8);
+  float r = 0.f;
+  if (lane < 8) {
+    r = a[lane];
+    for (int q = lane + 8; q < n8; q += 8) r += a[q];
+  }
+  auto rl = [&](int k) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), k)); };
+  float res = ((rl(0) + rl(1)) + (rl(2) + rl(3))) + ((rl(4) + rl(5)) + (rl(6) + rl(7)));
+  for (int q = n8; q < n; ++q) res += a[q];
+  return res;
+}
+
+// np_pairwise_f32 over one wave (n <= 256: at most one split)
+__device__ __forceinline__ float wave_pairwise_f32(const float* a, int n) {
+  if (n <= 128) return wave_pw_block_f32(a, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return wave_pw_block_f32(a, n2) + wave_pw_block_f32(a + n2, n - n2);
+}
+
 // `rounds` Krum selections over a shrinking alive set (rounds = 1: plain krum).
 // order[t] = client chosen in round t; scores (round 0, all N) optional.
-__global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restrict__ S, const int* __restrict__ J,
+// One workgroup of 16 waves.  For N <= 128 the sorted rows (S fp32, J as
+// bytes) are staged in LDS once, so a round is LDS-only.  Per round a wave
+// takes its alive rows eight at a time: a ballot compaction of each row's
+// first m alive entries, then the eight rows' pairwise sums at once (lanes
+// 8u..8u+7 run row u's eight accumulators, lane 8u combines them and adds the
+// tail), then a wave-parallel first minimum.  (Round 1 summed on one lane per
+// row from global memory: 2.5 ms for Bulyan's 88 rounds at N = 128.)
+constexpr int kKrumGStaged = 128;   // compacted-row stride (m <= 125 for N <= 128)
+constexpr int kKrumGGlobal = 256;
+
+template <bool STAGED>
+__global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restrict__ Sg, const int* __restrict__ Jg,
                                                            int n, int f, int rounds, int* __restrict__ order,
                                                            float* __restrict__ scores0, int* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) char kr_smem[];
+  constexpr int GS = STAGED ? kKrumGStaged : kKrumGGlobal;
   __shared__ unsigned char alive[kMaxClients];
   __shared__ float score[kMaxClients];
-  __shared__ float gath[16][kMaxClients];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int nwaves = blockDim.x >> 6;
+  float* gath = reinterpret_cast<float*>(kr_smem);                            // [16][8][GS]
+  float* Ss = gath + 16 * 8 * GS;                                            // [n][n] when staged
+  unsigned char* Js = reinterpret_cast<unsigned char*>(Ss + (STAGED ? n * n : 0));
+  if constexpr (STAGED) {
+    for (int e = tid; e < n * n; e += blockDim.x) {
+      Ss[e] = Sg[e];
+      Js[e] = static_cast<unsigned char>(Jg[e]);
+    }
+  }
   for (int i = tid; i < n; i += blockDim.x) alive[i] = 1;
   __syncthreads();
+  float* gw = gath + wave * 8 * GS;
+  const int u_me = lane >> 3, k_me = lane & 7;
   for (int t = 0; t < rounds; ++t) {
     const int nr = n - t;
     const int m = slice_count(nr - f - 2, nr - 1);
-    for (int i = wave; i < n; i += nwaves) {
-      if (!alive[i]) continue;  // wave-uniform
-      // compact the first m alive entries of sorted row i into gath[wave]
-      int c = 0;
-      for (int p0 = 0; p0 < n - 1 && c < m; p0 += 64) {
-        const int p = p0 + lane;
-        const bool ok = p < n - 1 && alive[J[(int64_t)i * n + p]];
-        const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
-        const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
-        if (ok && c + pre < m) gath[wave][c + pre] = S[(int64_t)i * n + p];
-        c += __builtin_popcountll(bal);
+    for (int u0 = 0; wave + nwaves * u0 < n; u0 += 8) {
+      // compaction of up to eight rows
+#pragma unroll 1
+      for (int u = 0; u < 8; ++u) {
+        const int i = wave + nwaves * (u0 + u);
+        if (i >= n || !alive[i]) continue;   // wave-uniform
+        int c = 0;
+        for (int p0 = 0; p0 < n - 1 && c < m; p0 += 64) {
+          const int p = p0 + lane;
+          const int64_t e = static_cast<int64_t>(i) * n + p;
+          const bool ok = p < n - 1 && alive[STAGED ? Js[e] : Jg[e]];
+          const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
+          const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
+          if (ok && c + pre < m) gw[u * GS + c + pre] = STAGED ? Ss[e] : Sg[e];
+          c += __builtin_popcountll(bal);
+        }
       }
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
-      if (lane == 0) score[i] = np_pairwise_f32<3>(gath[wave], m);
+      // numpy pairwise sums of the eight compacted rows
+      const int i_me = wave + nwaves * (u0 + u_me);
+      const bool row_ok = i_me < n && alive[i_me];
+      const float* a = gw + u_me * GS;
+      float sc = 0.f;
+      if (m <= 128) {
+        const int n8 = m - (m % 8);
+        float r = 0.f;
+        if (m >= 8 && row_ok) {
+          r = a[k_me];
+          for (int q = k_me + 8; q < n8; q += 8) r += a[q];
+        }
+        const int g = lane & ~7;
+        const float r1 = __shfl(r, g + 1), r2 = __shfl(r, g + 2), r3 = __shfl(r, g + 3);
+        const float r4 = __shfl(r, g + 4), r5 = __shfl(r, g + 5), r6 = __shfl(r, g + 6), r7 = __shfl(r, g + 7);
+        if (k_me == 0 && row_ok) {
+          if (m < 8) {
+            for (int q = 0; q < m; ++q) sc += a[q];
+          } else {
+            sc = ((r + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+            for (int q = n8; q < m; ++q) sc += a[q];
+          }
+          score[i_me] = sc;
+        }
+      } else {
+        // N > 130: one row at a time over the whole wave (numpy's split at n/2)
+#pragma unroll 1
+        for (int u = 0; u < 8; ++u) {
+          const int i = wave + nwaves * (u0 + u);
+          if (i >= n || !alive[i]) continue;
+          const float v = wave_pairwise_f32(gw + u * GS, m);
+          if (lane == 0) score[i] = v;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    if (tid == 0) {
-      // np.argmin: first minimum; a NaN is the minimum (first NaN wins)
-      int best = -1;
+    if (wave == 0) {
+      // np.argmin: first minimum; a NaN is the minimum (first NaN wins).
+      // key: (class 0 NaN / 1 number / 2 dead, value, index)
+      int bc = 2, bi = 0x7fffffff;
       float bv = 0.f;
-      for (int i = 0; i < n; ++i) {
-        if (!alive[i]) continue;
+      for (int i = lane; i < n; i += 64) {
         const float v = score[i];
-        if (best < 0) { best = i; bv = v; if (v != v) break; continue; }
-        if (v != v) { best = i; break; }
-        if (v < bv) { best = i; bv = v; }
+        const int c = !alive[i] ? 2 : (v != v ? 0 : 1);
+        if (c < bc || (c == bc && c == 1 && v < bv)) {   // i ascends per lane: ties keep the first
+          bc = c;
+          bv = v;
+          bi = i;
+        }
       }
-      order[t] = best;
-      if (best >= 0) alive[best] = 0;
-      if (best < 0 && status) *status = 1;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const int oc = __shfl_xor(bc, off);
+        const float ov = __shfl_xor(bv, off);
+        const int oi = __shfl_xor(bi, off);
+        const bool better = oc < bc || (oc == bc && ((oc == 1 && ov < bv) || ((oc != 1 || ov == bv) && oi < bi)));
+        if (better) {
+          bc = oc;
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (lane == 0) {
+        const int best = bc < 2 ? bi : -1;
+        order[t] = best;
+        if (best >= 0) alive[best] = 0;
+        if (best < 0 && status) *status = 1;
+      }
     }
     if (t == 0 && scores0) {
-      __syncthreads();
       for (int i = tid; i < n; i += blockDim.x) scores0[i] = score[i];
     }
     __syncthreads();
@@ -207,7 +317,23 @@ int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int*
     rc = launch_status("krum_rowsort_kernel");
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(krum_rounds_kernel, dim3(1), dim3(1024), 0, s, S, J, n, f, rounds, order, scores0, nullptr);
+  if (n <= 128) {
+    const int lds = 16 * 8 * kKrumGStaged * 4 + n * n * 5;   // compacted rows + S fp32 + J bytes
+    static const hipError_t attr =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(krum_rounds_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 8 * kKrumGStaged * 4 + 128 * 128 * 5);
+    if (attr == hipSuccess) {
+      hipLaunchKernelGGL(krum_rounds_kernel<true>, dim3(1), dim3(1024), lds, s, S, J, n, f, rounds, order, scores0,
+                         nullptr);
+      return launch_status("krum_rounds_kernel");
+    }
+  }
+  static const hipError_t attr_g =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(krum_rounds_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 8 * kKrumGGlobal * 4);
+  (void)attr_g;
+  hipLaunchKernelGGL(krum_rounds_kernel<false>, dim3(1), dim3(1024), 16 * 8 * kKrumGGlobal * 4, s, S, J, n, f, rounds,
+                     order, scores0, nullptr);
   return launch_status("krum_rounds_kernel");
 }
 

@@ -186,6 +186,19 @@ def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
     return (out, sel) if selected else out
 
 
+def bulyan_stage(S, beta):
+    """The per-coordinate Bulyan stage over the rows of a (theta, d) float32
+    device matrix in selection order (robust_estimator.py:324-330): (d,)
+    float64.  beta = theta - 2f (Python slice semantics when negative)."""
+    S, theta, d, lds = as_matrix(S)
+    out = torch.empty(d, dtype=torch.float64, device=S.device)
+    nb = _lib.query_bytes("sra_bulyan_stage_workspace_bytes", theta, d)
+    ws = _workspace(nb, S.device)
+    _lib.call("sra_bulyan_stage_f32", S.data_ptr(), theta, d, lds, int(beta), out.data_ptr(), ws.data_ptr(), nb,
+              _stream_ptr(S.device))
+    return out
+
+
 def bulyan_coordinates(A, beta, median_index=False, median_row=False):
     """The per-coordinate Bulyan stage over the columns of a (theta, d) float64
     device matrix (robust_estimator.py:259-275 for every column): returns the

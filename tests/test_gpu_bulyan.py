@@ -82,6 +82,50 @@ def test_bulyan_even_theta_tiebreak_dense_ties():
         np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)
 
 
+@pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
+def test_bulyan_wide_magnitude_columns(mode):
+    """Columns whose values span more than fp64 can sum exactly (1e-2 beside
+    1e-12 and 1e-30) take the listed-column path: numpy's pairwise totals for
+    the centre and the argsort-order walk for the window."""
+    rng = np.random.default_rng(17)
+    x = (0.01 * rng.standard_normal((40, 600))).astype(np.float32)
+    cols = rng.choice(600, 200, replace=False)
+    for c in cols:
+        rows = rng.choice(40, 3, replace=False)
+        x[rows[0], c] *= 1e-10
+        x[rows[1], c] *= 1e-28
+    want, _ = _leftfirst_and_ties(list(x), 8, mode)
+    got = engine.bulyan(torch.from_numpy(x).cuda(), 8, mode).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15, equal_nan=True)
+
+
+@pytest.mark.parametrize("theta,beta", [(88, 48), (22, 4), (31, 5), (16, -8), (10, -10), (128, 40), (7, 7)])
+def test_stage_f32_columns(theta, beta):
+    """The per-coordinate stage alone (sra_bulyan_stage_f32) on float32 rows:
+    plain columns, wide-magnitude columns (listed path), NaN / inf columns
+    (the generic stage), duplicate-heavy columns, against the left-first
+    restatement of robust_estimator.py:259-275."""
+    rng = np.random.default_rng(theta * 7 + beta)
+    d = 900
+    S = (0.01 * rng.standard_normal((theta, d))).astype(np.float32)
+    S[:, 100:200] = rng.integers(-3, 4, size=(theta, 100)).astype(np.float32)   # ties
+    for c in range(200, 300):
+        r = rng.choice(theta, 2, replace=False)
+        S[r[0], c] *= 1e-12
+        S[r[1], c] *= 1e-30
+    S[rng.integers(0, theta), 300] = np.nan
+    S[rng.integers(0, theta), 301] = np.inf
+    S[rng.integers(0, theta), 302] = -np.inf
+    S[:2, 303] = np.inf
+    S[:, 304] = 0.0
+    got = engine.bulyan_stage(torch.from_numpy(S).cuda(), beta).cpu().numpy()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j].astype(np.float64), beta) for j in range(d)])
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15, equal_nan=True)
+
+
 def test_scalar_helpers_match_reference():
     """Drop-in bulyan_median / bulyan_one_coordinate (robust_estimator.py:259-275)
     against the live-reference fixture (float64 in, numpy scalars out)."""
