@@ -133,9 +133,9 @@ KERNEL_NAME = {
     "trimmedmean": "select_plain_kernel<1, 128, 12>",
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
-    "krum": "whole krum op (gram_partial_kernel dominant; per-kernel split in profiles/)",
-    "mom_krum": "whole mom_krum op (bucket means + Gram + scoring)",
-    "bulyankrum": "whole bulyan op (Gram + theta Krum rounds + final stage)",
+    "krum": "whole krum op (bf16x3 gram_partial_kernel dominant; per-kernel split in profiles/)",
+    "mom_krum": "whole mom_krum op (bucket means + bf16x3 Gram + scoring)",
+    "bulyankrum": "whole bulyan op (bf16x3 Gram + theta Krum rounds + final stage)",
     "bulyanmedian": "whole bulyan op (theta select+distance rounds + final stage)",
     "bulyantrimmedmean": "whole bulyan op (theta select+distance rounds + final stage)",
     "filterl2": "spectral_filter_kernel<0> (chunk Gram on fp64 MFMA + client-space solver)",
@@ -167,9 +167,17 @@ def roofline_model(agg, n, d):
     """(bound, peak, unit, algorithmic amount per launch) — SURVEY.md §8(d)."""
     if agg in ("trimmedmean", "median", "average", "dba_median", "dba_weighted_sum"):
         return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
-    if agg in ("krum", "mom_krum", "bulyankrum"):
-        m = n if agg != "mom_krum" else -(-n // 3)
-        return "mfma", MFMA_PEAK_TFLOPS, "TFLOP/s", m * (m + 1) * d
+    # Krum family: the Gram runs on the bf16 MFMA with a three-way split (six
+    # bf16 32x32x16 per tile and k-step, ~0.5 ms per 1e7 coordinates at N=128
+    # at the 2.5 PF peak) and is bound by streaming X once: bytes, not flops
+    if agg == "krum":
+        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d
+    if agg == "mom_krum":
+        m = -(-n // 3)
+        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 2 * 4 * m * d   # buckets: read X, write + re-read means
+    if agg == "bulyankrum":
+        theta = n - 40
+        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * theta * d + 8 * d   # Gram, final stage, out
     if agg in ("bulyanmedian", "bulyantrimmedmean"):
         theta = n - 40
         return "hbm", HBM_PEAK_GBS, "GB/s", 4 * d * sum(n - i for i in range(theta)) + 8 * theta * d + 4 * d

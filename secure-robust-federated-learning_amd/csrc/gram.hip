@@ -1,33 +1,45 @@
 // k2 — centred pairwise Gram matrix G = Xc Xc^T (N x N, fp64 result) on the
-// fp32 MFMA (v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulate).
+// bf16 MFMA with a three-way split of every fp32 value (v_mfma_f32_32x32x16_bf16).
 //
 // Feeds every pairwise-L2 consumer of the reference:
 //   krum_ / krum / mom_krum  (src/robust_estimator.py:234-257)
 //   bulyan(aggsubfunc='krum') (src/robust_estimator.py:286-296)
 // through ||x_i - x_j||^2 = G_ii + G_jj - 2 G_ij.
 //
-// Centring: before the MFMA every 64-coordinate stage is shifted by its
-// per-coordinate client mean (distances are translation invariant), which
-// removes the cancellation of the expanded form when clients share a large
-// common component.  All (i, j) entries accumulate their products in the same
-// k order, so two identical clients get G_ii == G_jj == G_ij bit for bit and
+// Centring: before the MFMA every stage is shifted by its per-coordinate
+// client mean (distances are translation invariant), which removes the
+// cancellation of the expanded form when clients share a large common
+// component.  All (i, j) entries accumulate their products in the same k
+// order, so two identical clients get G_ii == G_jj == G_ij bit for bit and
 // distance exactly 0, as in the reference (identical rows of the `xie`
 // attack, src/attack.py:362-372).
 //
-// Layout / schedule (one 256-thread workgroup per CU, persistent over a
-// contiguous coordinate range so every row is streamed contiguously):
-//   stage = NP rows x 64 coordinates, register-staged float4 loads (one stage
-//   ahead) -> LDS [row][64 + 4 pad] (conflict-free ds_read_b128), double
-//   buffered; per-stage column means from the staging registers.
+// Precision: each centred fp32 value x is split exactly into three bf16
+// parts x = h + m + l (round-to-nearest h, then m of the remainder, then l of
+// what is left: 8 + 8 + 8 significant bits); the product x y is formed from
+// the six terms hh + hm + mh + hl + lh + mm on the bf16 MFMA (exact products,
+// fp32 accumulation), dropping ml + lm + ll (< 3 * 2^-24 of |x y|) -- the
+// accuracy of an fp32 product -- at 16x the fp32 MFMA's rate: six bf16
+// MFMAs cost 3/8 of one fp32 32x32x2 pass over the same k, so the kernel is
+// bound by HBM instead of the fp32 MFMA (round 1: 2.15 ms at N=128, d=1e7).
+//
+// Layout / schedule (one workgroup of 4 or 8 waves per CU, persistent;
+// workgroup w takes coordinate tiles w, w + #WG, ... so the chip streams
+// neighbouring tiles of every row at once):
+//   stage = NP rows x STAGE coordinates, register-staged float4 loads (one
+//   stage ahead) -> LDS [row][STAGE + 4 pad], double buffered; per-wave column
+//   partial sums from the staging registers, reduced to the stage's column
+//   means in a fixed order after the stage barrier.
 //   wave w owns a set of upper-triangle 32x32 output tiles (I <= J) and a
-//   subset of the 8-coordinate groups (K split across waves when the tile
-//   count is small).  One ds_read_b128 per row block gives the A/B fragments
-//   of 4 MFMA k-steps (k order permuted identically for A and B).
+//   subset of the 16-coordinate k-steps (K split across waves).  Two
+//   ds_read_b128 per row block give a lane its 8 values of a k-step; centre
+//   by the stage means, split, six MFMAs per tile.
 //   Partial tiles go to a slab [wg][kgroup][tile][32x32]; gram_reduce sums the
 //   slab in a fixed order in fp64 (deterministic) and mirrors to N x N.
 //
-// Roofline at N=128 (10 tiles): 2*8256*d flops on MFMA vs 4*N*d bytes: MFMA
-// bound (~1.05 ms per 1e7 coordinates at the 157 TF fp32 MFMA peak).
+// Roofline at N=128: 4*N*d bytes streamed once; the MFMA work (6 bf16
+// 32x32x16 per tile and k-step, 10 tiles) is ~0.5 ms per 1e7 coordinates at
+// the 2.5 PF bf16 peak, below the ~0.8 ms of HBM time.
 #include "sra_common.hpp"
 
 #include <cstdlib>
@@ -35,6 +47,22 @@
 namespace sra {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// exact three-way bf16 split of 8 fp32 values: x = h + m + l
+__device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
+  float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 hh = static_cast<__bf16>(x[e]);
+    const float r1 = x[e] - static_cast<float>(hh);
+    const __bf16 mm = static_cast<__bf16>(r1);
+    const float r2 = r1 - static_cast<float>(mm);
+    h[e] = hh;
+    m[e] = mm;
+    l[e] = static_cast<__bf16>(r2);
+  }
+}
 
 template <int NB, int WAVES = 4>
 struct GramCfg {
@@ -49,8 +77,8 @@ struct GramCfg {
                                        : (NB <= 3 ? 1 : (NB <= 5 ? 2 : (NB <= 7 ? 4 : 8)));
   static constexpr int WK = WAVES / WT;                          // k groups
   static constexpr int TPW = (T + WT - 1) / WT;                  // tiles per wave (max)
-  static constexpr int GROUPS = STAGE / 8;                       // 8-coordinate groups per stage
-  static constexpr int GPW = GROUPS / WK;                        // groups per wave per stage
+  static constexpr int KSTEPS = STAGE / 16;                      // 16-coordinate k-steps per stage
+  static constexpr int KPW = KSTEPS / WK;                        // k-steps per wave per stage
   static constexpr int C4 = STAGE / 4;                           // float4 columns per row
   static constexpr int RSTEP = THREADS / C4;                     // rows covered per load sweep
   static constexpr int LOADS = NP / RSTEP > 0 ? NP / RSTEP : 1;  // float4 per thread per stage
@@ -74,7 +102,7 @@ struct GramCfg {
   }
   static constexpr int BUF = NP * ROWPAD;                        // floats per stage buffer
   static constexpr int PART = WAVES * STAGE;                     // per-wave column partials
-  static constexpr int lds_floats = 2 * BUF + 2 * PART;
+  static constexpr int lds_floats = 2 * BUF + PART + 2 * STAGE;  // stage buffers, partials, means
 };
 
 template <int NB, int WAVES>
@@ -102,15 +130,20 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
   // LDS carve-up (pointers derived arithmetically from the __shared__ base so
   // the compiler keeps them in the LDS address space: ds_read/ds_write)
   auto bufp = [&](int which) { return lds + which * C::BUF; };
-  auto partp = [&](int which) { return lds + 2 * C::BUF + which * C::PART; };
+  float* part = lds + 2 * C::BUF;
+  auto mup = [&](int which) { return lds + 2 * C::BUF + C::PART + which * STAGE; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int kg = wave / C::WT;
-  const int64_t k_begin = static_cast<int64_t>(blockIdx.x) * chunk;
-  const int64_t k_end = k_begin + chunk < d ? k_begin + chunk : d;
-  const int nstage = k_begin < k_end ? static_cast<int>(cdiv(k_end - k_begin, STAGE)) : 0;
+  // stage s of this workgroup = coordinate tile s * gridDim.x + blockIdx.x: all
+  // workgroups stream neighbouring tiles of the N rows at any moment (a
+  // contiguous chunk per workgroup kept N x #WG pages open at once)
+  (void)chunk;
+  const int64_t ntiles = cdiv(d, STAGE);
+  const int nstage = blockIdx.x < ntiles ? static_cast<int>(cdiv(ntiles - blockIdx.x, gridDim.x)) : 0;
+  const int64_t k_end = d;
   const float inv_n = 1.0f / static_cast<float>(n);
 
   f32x16 acc[C::TPW];
@@ -125,7 +158,7 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
   const int row0 = tid / C::C4;
 
   auto load_stage = [&](int s) {
-    const int64_t k0 = k_begin + static_cast<int64_t>(s) * STAGE + 4 * c4;
+    const int64_t k0 = (static_cast<int64_t>(s) * gridDim.x + blockIdx.x) * STAGE + 4 * c4;
 #pragma unroll
     for (int q = 0; q < C::LOADS; ++q) {
       const int row = row0 + C::RSTEP * q;
@@ -166,10 +199,22 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
     }
   };
 
+  // column means of a stored stage: fixed order over the waves' partials
+  auto stage_means = [&](float* mu) {
+    for (int c = tid; c < STAGE; c += C::THREADS) {
+      float m = part[c];
+#pragma unroll
+      for (int w = 1; w < WAVES; ++w) m += part[w * STAGE + c];
+      mu[c] = m * inv_n;
+    }
+  };
+
   if (nstage > 0) {
     load_stage(0);
-    store_stage(bufp(0), partp(0));
+    store_stage(bufp(0), part);
     if (nstage > 1) load_stage(1);
+    __syncthreads();
+    stage_means(mup(0));
     __syncthreads();
   }
 
@@ -179,38 +224,50 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
   const float last_mask = (32 * (NB - 1) + r) < n ? 1.f : 0.f;
   for (int s = 0; s < nstage; ++s) {
     const float* b = bufp(s & 1);
-    const float* part = partp(s & 1);
-    // ---- MFMA over this wave's 8-coordinate groups of the stage ----
+    const float* mu = mup(s & 1);
+    // ---- MFMA over this wave's 16-coordinate k-steps of the stage ----
 #pragma unroll
-    for (int gi = 0; gi < C::GPW; ++gi) {
+    for (int gi = 0; gi < C::KPW; ++gi) {
       const int g = kg + C::WK * gi;
-      const int col = 8 * g + 4 * h;
-      f32x4 mu = *reinterpret_cast<const f32x4*>(part + col);
+      const int col = 16 * g + 8 * h;
+      const f32x4 mu0 = *reinterpret_cast<const f32x4*>(mu + col);
+      const f32x4 mu1 = *reinterpret_cast<const f32x4*>(mu + col + 4);
+      bf16x8 fh[NB], fm[NB], fl[NB];
 #pragma unroll
-      for (int w = 1; w < WAVES; ++w) mu += *reinterpret_cast<const f32x4*>(part + w * STAGE + col);
-      mu *= inv_n;
-      f32x4 fr[NB];
-#pragma unroll
-      for (int blk = 0; blk < NB; ++blk)
-        fr[blk] = *reinterpret_cast<const f32x4*>(b + (32 * blk + r) * C::ROWPAD + col) - mu;
-      fr[NB - 1] *= last_mask;
+      for (int blk = 0; blk < NB; ++blk) {
+        const float* rp = b + (32 * blk + r) * C::ROWPAD + col;
+        f32x4 a0 = *reinterpret_cast<const f32x4*>(rp) - mu0;
+        f32x4 a1 = *reinterpret_cast<const f32x4*>(rp + 4) - mu1;
+        if (blk == NB - 1) {
+          a0 *= last_mask;
+          a1 *= last_mask;
+        }
+        split3(a0, a1, fh[blk], fm[blk], fl[blk]);
+      }
 #pragma unroll
       for (int t = 0; t < C::TPW; ++t) {
         const int tile = tg + C::WT * t;     // compile-time: tg is a template parameter
         if (tile < C::T) {
           const int ti = C::kTileI(tile), tj = C::kTileJ(tile);
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[ti][ks], fr[tj][ks], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[ti], fh[tj], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[ti], fm[tj], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm[ti], fh[tj], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[ti], fl[tj], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[ti], fh[tj], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm[ti], fm[tj], acc[t], 0, 0, 0);
         }
       }
     }
     // ---- stage s+1 -> LDS (its registers were loaded one stage ahead) ----
     if (s + 1 < nstage) {
-      store_stage(bufp((s + 1) & 1), partp((s + 1) & 1));
+      store_stage(bufp((s + 1) & 1), part);
       if (s + 2 < nstage) load_stage(s + 2);
     }
     __syncthreads();
+    if (s + 1 < nstage) {
+      stage_means(mup((s + 1) & 1));
+      __syncthreads();
+    }
   }
 
   // ---- partial tiles -> slab[wg][kg][tile][32 x 32] (row-major) ----
@@ -300,12 +357,18 @@ int gram_num_wg(int64_t d) {
   return static_cast<int>(stages < 256 ? (stages > 0 ? stages : 1) : 256);
 }
 
-static int gram_waves() {
-  static const int w = [] {
+// 4 waves (one per SIMD, all tiles of a k-step in one wave: the fragments are
+// centred and split once per wave) for N <= 128 -- measured 1.43 vs 1.50 ms
+// for 8 waves at N = 128, d = 1e7; 8 waves for larger N (the 4-wave tile
+// groups would need more accumulators than a wave holds).  SRA_GRAM_WAVES=4|8
+// overrides, for A/B runs.
+static int gram_waves(int nb) {
+  static const int force = [] {
     const char* e = getenv("SRA_GRAM_WAVES");
-    return (e != nullptr && atoi(e) == 4) ? 4 : 8;
+    return e != nullptr ? atoi(e) : 0;
   }();
-  return w;
+  if (force == 4 || force == 8) return force;
+  return nb <= 4 ? 4 : 8;
 }
 
 template <int NB, int WAVES>
@@ -339,7 +402,7 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
 
 template <int NB>
 static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s) {
-  if (gram_waves() == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s);
+  if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s);
   return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s);
 }
 
