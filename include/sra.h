@@ -139,6 +139,24 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
                    int32_t* selected, void* ws, size_t ws_bytes, void* stream);
 
 
+/* One selection round of Bulyan's median / trimmed-mean modes
+ * (src/robust_estimator.py:297-322) over the listed clients rows[0, nr) of an
+ * N x d block (a whole layer or a column shard of it): agg (d floats) = the
+ * coordinate-wise median (mode 1) or trimmed mean (mode 2; dba != 0: the DBA
+ * harness's lower median, src/DBA/helper.py:1025) of the listed rows; dist[r]
+ * (nr doubles) = squared L2 distance of listed row r to agg over this block's
+ * columns.  Column shards' dist vectors sum to the full distance.  N <= 128;
+ * workspace from sra_bulyan_round_workspace_bytes. */
+int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes);
+int sra_bulyan_round_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const int32_t* rows, int32_t nr,
+                         int32_t mode, int32_t dba, float* agg, double* dist, void* ws, size_t ws_bytes,
+                         void* stream);
+/* The round's pick: the first strict minimum of dist (NaN never chosen; all
+ * NaN / inf -> *status = 1, the reference's AssertionError) is removed from
+ * rows[0, nr) into rows_next[0, nr - 1), order preserved. */
+int sra_bulyan_pick(const double* dist, const int32_t* rows, int32_t nr, int32_t* rows_next, int32_t* status,
+                    void* stream);
+
 /* The per-coordinate Bulyan stage alone on theta float32 rows (row i = the
  * i-th selected vector in selection order, row stride lds): out[j] (float64)
  * as sra_bulyan_f32's final stage computes it for robust_estimator.py:324-330

@@ -276,19 +276,21 @@ __global__ void __launch_bounds__(256) row_dist_multi_kernel(const float* __rest
     partial[static_cast<int64_t>(rp0 + threadIdx.x) * kDistChunks + c] = red[threadIdx.x][0];
 }
 
+// fp64 distance of every listed row: its chunk partials summed in chunk order
+__global__ void __launch_bounds__(256) bulyan_dist_kernel(const float* __restrict__ partial, int nr, int nchunks,
+                                                          double* __restrict__ dist) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  double s = 0.0;
+  for (int c = 0; c < nchunks; ++c) s += static_cast<double>(partial[static_cast<int64_t>(r) * kDistChunks + c]);
+  dist[r] = s;
+}
+
 // argmin (first strict minimum, NaN never chosen) of the listed rows'
 // distances; removes it from the list (order preserved) into rows_next.
-__global__ void __launch_bounds__(256) bulyan_pick_kernel(const float* __restrict__ partial, const int* __restrict__ rows,
-                                                         int nr, int nchunks, int* __restrict__ rows_next,
-                                                         int* __restrict__ status) {
-  __shared__ double dist[kMaxClientsBulyan];
+__global__ void __launch_bounds__(256) bulyan_pick_kernel(const double* __restrict__ dist, const int* __restrict__ rows,
+                                                         int nr, int* __restrict__ rows_next, int* __restrict__ status) {
   __shared__ int pick;
-  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
-    double s = 0.0;
-    for (int c = 0; c < nchunks; ++c) s += static_cast<double>(partial[static_cast<int64_t>(r) * kDistChunks + c]);
-    dist[r] = s;
-  }
-  __syncthreads();
   if (threadIdx.x == 0) {
     int best = -1;
     double bv = __builtin_inf();
@@ -297,7 +299,7 @@ __global__ void __launch_bounds__(256) bulyan_pick_kernel(const float* __restric
       if (dist[r] < bv) { bv = dist[r]; best = r; }
     }
     pick = best;
-    if (best < 0) *status = 1;  // AssertionError in the reference (all NaN)
+    if (best < 0 && status) *status = 1;  // AssertionError in the reference (all NaN / inf)
   }
   __syncthreads();
   const int p = pick < 0 ? 0 : pick;
@@ -745,7 +747,7 @@ static size_t bulyan_body_bytes(int n, int64_t d, int mode, int f) {
     b += krum_workspace_bytes(n, d);
   } else {
     b += sizeof(float) * static_cast<size_t>(theta > 0 ? theta : 0) * static_cast<size_t>(d) + 256;
-    b += sizeof(float) * static_cast<size_t>(n) * kDistChunks;
+    b += sizeof(float) * static_cast<size_t>(n) * kDistChunks + sizeof(double) * static_cast<size_t>(n) + 256;
   }
   return (b + 255) / 256 * 256;
 }
@@ -799,6 +801,42 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int theta
   return rc;
 }
 
+// One selection round of Bulyan's median / trimmed-mean modes
+// (robust_estimator.py:297-322) over the listed rows: agg = the coordinate-wise
+// aggregate of the remaining clients, dist[r] = squared L2 distance of listed
+// row r to it (fp32 within each of kDistChunks coordinate chunks, fp64 across
+// them in chunk order).  Over a column shard, dist is this shard's share: the
+// shards' dist vectors sum (all-reduce) to the distance over all columns.
+static int launch_bulyan_round(const float* X, int64_t d, int64_t ldx, const int* rows, int nr, int mode, bool dba,
+                               float* agg, float* partial, double* dist, hipStream_t s) {
+  int rc;
+  if (mode == kBulyanMedian && dba) {
+    const int k = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
+    rc = launch_select_rows<1>(X, ldx, rows, nr, d, k, k + 1, agg, s);
+  } else if (mode == kBulyanMedian) {
+    rc = launch_select_rows<0>(X, ldx, rows, nr, d, 0, nr, agg, s);
+  } else {
+    const int b = static_cast<int>(nr * 0.1);  // trimmed_mean(beta=0.1): int(size * beta)
+    const int lo = b, hi = nr - b > b ? nr - b : b;
+    rc = launch_select_rows<1>(X, ldx, rows, nr, d, lo, hi, agg, s);
+  }
+  if (rc) return rc;
+  const int64_t chunk = cdiv(cdiv(d, kDistChunks), 4) * 4;
+  const int nchunks = static_cast<int>(cdiv(d, chunk));
+  const bool dist_vec = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && (ldx % 4 == 0) && (d % 4 == 0) &&
+                        (reinterpret_cast<uintptr_t>(agg) % 16 == 0);
+  if (dist_vec)
+    hipLaunchKernelGGL(row_dist_multi_kernel<4>, dim3(nchunks, cdiv(nr, 4)), dim3(256), 0, s, X, ldx, rows, nr, d,
+                       agg, chunk, partial);
+  else
+    hipLaunchKernelGGL(row_dist_partial_kernel<false>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, rows, d, agg,
+                       chunk, partial);
+  rc = launch_status("row_dist_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bulyan_dist_kernel, dim3(cdiv(nr, 256)), dim3(256), 0, s, partial, nr, nchunks, dist);
+  return launch_status("bulyan_dist_kernel");
+}
+
 __global__ void iota_kernel(int* p, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = i;
@@ -838,34 +876,16 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   hipLaunchKernelGGL(iota_kernel, dim3(cdiv(theta, 256)), dim3(256), 0, s, order, theta);
   rc = launch_status("iota_kernel");
   if (rc) return rc;
-  const int64_t chunk = cdiv(cdiv(d, kDistChunks), 4) * 4;
-  const int nchunks = static_cast<int>(cdiv(d, chunk));
-  const bool dist_vec = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && (ldx % 4 == 0) && (d % 4 == 0);
+  double* dist = reinterpret_cast<double*>(
+      (reinterpret_cast<uintptr_t>(partial + static_cast<size_t>(n) * kDistChunks) + 255) & ~static_cast<uintptr_t>(255));
   int* cur = rows_a;
   int* nxt = rows_b;
   for (int t = 0; t < theta; ++t) {
     const int nr = n - t;
     float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
-    if (mode == kBulyanMedian && dba) {
-      const int k = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
-      rc = launch_select_rows<1>(X, ldx, cur, nr, d, k, k + 1, agg, s);
-    } else if (mode == kBulyanMedian) {
-      rc = launch_select_rows<0>(X, ldx, cur, nr, d, 0, nr, agg, s);
-    } else {
-      const int b = static_cast<int>(nr * 0.1);  // trimmed_mean(beta=0.1): int(size * beta)
-      const int lo = b, hi = nr - b > b ? nr - b : b;
-      rc = launch_select_rows<1>(X, ldx, cur, nr, d, lo, hi, agg, s);
-    }
+    rc = launch_bulyan_round(X, d, ldx, cur, nr, mode, dba, agg, partial, dist, s);
     if (rc) return rc;
-    if (dist_vec)
-      hipLaunchKernelGGL(row_dist_multi_kernel<4>, dim3(nchunks, cdiv(nr, 4)), dim3(256), 0, s, X, ldx, cur, nr, d,
-                         agg, chunk, partial);
-    else
-      hipLaunchKernelGGL(row_dist_partial_kernel<false>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, cur, d, agg,
-                         chunk, partial);
-    rc = launch_status("row_dist_partial_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, partial, cur, nr, nchunks, nxt, status);
+    hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, dist, cur, nr, nxt, status);
     rc = launch_status("bulyan_pick_kernel");
     if (rc) return rc;
     int* tmp = cur;
@@ -946,4 +966,38 @@ extern "C" int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, in
   const int rc = launch_status("iota_kernel");
   if (rc) return rc;
   return launch_final(S, lds, rows, static_cast<int>(theta), beta, d, out, nf_count, nf_list, s);
+}
+
+// One Bulyan selection round over a (possibly column-sharded) N x d block, for
+// a caller that sums the shards' distances (all-reduce) and picks itself.
+extern "C" int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && n <= 128, SRA_ERR_UNSUPPORTED, "bulyan rounds support 1 <= N <= 128");
+  *bytes = sizeof(float) * static_cast<size_t>(n) * kDistChunks + 256;
+  return SRA_OK;
+}
+
+extern "C" int sra_bulyan_round_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const int32_t* rows,
+                                    int32_t nr, int32_t mode, int32_t dba, float* agg, double* dist, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && rows != nullptr && agg != nullptr && dist != nullptr && ws != nullptr, SRA_ERR_ARG,
+              "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= 128 && nr >= 1 && nr <= n && d >= 1 && ldx >= d, SRA_ERR_SHAPE,
+              "bad shape (N <= 128, 1 <= nr <= N)");
+  SRA_REQUIRE(mode == kBulyanMedian || mode == kBulyanTrimmed, SRA_ERR_ARG, "round mode must be median (1) or "
+              "trimmedmean (2), got %d", mode);
+  size_t need = 0;
+  sra_bulyan_round_workspace_bytes(n, &need);
+  SRA_REQUIRE(ws_bytes >= need, SRA_ERR_WORKSPACE, "bulyan round workspace too small: need %zu bytes", need);
+  return launch_bulyan_round(X, d, ldx, rows, nr, mode, dba != 0, agg, static_cast<float*>(ws), dist,
+                             static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_bulyan_pick(const double* dist, const int32_t* rows, int32_t nr, int32_t* rows_next,
+                               int32_t* status, void* stream) {
+  SRA_REQUIRE(dist != nullptr && rows != nullptr && rows_next != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(nr >= 1, SRA_ERR_SHAPE, "nr >= 1");
+  hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), dist, rows, nr,
+                     rows_next, status);
+  return launch_status("bulyan_pick_kernel");
 }

@@ -186,6 +186,24 @@ def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
     return (out, sel) if selected else out
 
 
+def bulyan_round(X, rows, nr, aggsubfunc, agg, dist, dba=False):
+    """One Bulyan selection round (median / trimmedmean) over rows[:nr] of a
+    (shard of a) layer: fills agg (d float32) and dist (nr float64, squared
+    distances over this block's columns).  No host synchronisation."""
+    X, n, d, ldx = as_matrix(X)
+    mode = BULYAN_MODES[aggsubfunc]
+    nb = _lib.query_bytes("sra_bulyan_round_workspace_bytes", n)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_bulyan_round_f32", X.data_ptr(), n, d, ldx, rows.data_ptr(), int(nr), mode, int(bool(dba)),
+              agg.data_ptr(), dist.data_ptr(), ws.data_ptr(), nb, _stream_ptr(X.device))
+
+
+def bulyan_pick(dist, rows, nr, rows_next, status=None):
+    """Remove the first strict minimum of dist[:nr] from rows[:nr] into rows_next."""
+    _lib.call("sra_bulyan_pick", dist.data_ptr(), rows.data_ptr(), int(nr), rows_next.data_ptr(),
+              status.data_ptr() if status is not None else None, _stream_ptr(dist.device))
+
+
 def bulyan_stage(S, beta):
     """The per-coordinate Bulyan stage over the rows of a (theta, d) float32
     device matrix in selection order (robust_estimator.py:324-330): (d,)

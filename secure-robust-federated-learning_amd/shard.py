@@ -5,7 +5,7 @@ The gradient dimension d of a layer is split into contiguous column blocks;
 each rank reads only its N x d_r block:
 
 * coordinate-wise aggregators (average / median / trimmed mean, the Bulyan
-  final stage, bucket means) and the chunked spectral filters are
+  per-coordinate stage, bucket means) and the chunked spectral filters are
   independent per column (per itv-chunk for the filters, so filter shards are
   aligned to itv and restart chunking exactly where the single-GPU path
   does): every rank aggregates its block and one all-gather assembles the
@@ -15,7 +15,10 @@ each rank reads only its N x d_r block:
   mean), so each rank computes the Gram of its block and one all-reduce of
   N*N fp64 (128 KiB at N=128) sums them; scoring is N-space work done
   redundantly on every rank (identical inputs -> identical index), and the
-  chosen client's row is assembled with the same all-gather.
+  chosen client's row is assembled with the same all-gather;
+* Bulyan's median / trimmed-mean selection rounds: one all-reduce of the
+  <= N fp64 distance partials per round (the only per-round exchange), the
+  pick made identically on every rank, then the local per-coordinate stage.
 
 The helpers take the per-shard operations as arguments so that the sharding
 logic is exercised by world_size-2 gloo tests on CPU; the GPU path passes the
@@ -44,6 +47,8 @@ def all_bounds(d, world, align=1):
 
 
 def _world(group):
+    if not dist.is_initialized():   # a single process: the unsharded layer
+        return 1, 0
     return dist.get_world_size(group), dist.get_rank(group)
 
 
@@ -59,7 +64,7 @@ def gather_columns(local, d, align=1, group=None):
     lead = local.shape[:-1]
     padded = torch.zeros(lead + (width,), dtype=local.dtype, device=local.device)
     padded[..., :hi - lo] = local
-    if world == 1:
+    if not dist.is_initialized():
         return padded[..., :d].clone()
     gathered = torch.empty((world,) + lead + (width,), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(gathered, padded.unsqueeze(0).contiguous(), group=group)
@@ -80,12 +85,56 @@ def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
     select_fn(G, f) -> index of the chosen client (from the full Gram).
     Returns (full row of the chosen client, index)."""
     G = gram_fn(X_shard).to(torch.float64).contiguous()
-    world, _ = _world(group)
-    if world > 1:
+    if dist.is_initialized():   # (a 1-rank group still goes through the collective)
         dist.all_reduce(G, op=dist.ReduceOp.SUM, group=group)
     idx = int(select_fn(G, f))
     row = gather_columns(X_shard[idx], d, align, group)
     return row, idx
+
+
+def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
+    """Bulyan (robust_estimator.py:277-332) over a column-sharded layer.
+
+    The theta selection rounds need the distance of every remaining client to
+    the round's aggregate over ALL columns: each rank computes the aggregate
+    and the distances over its own columns (``ops["bulyan_round"]``), one
+    all-reduce of <= N fp64 partials per round sums them, and every rank
+    makes the same pick (``ops["bulyan_pick"]``) from the identical sums.
+    Krum mode: one all-reduce of the partial centred Gram, then the theta
+    Krum rounds redundantly on every rank (``ops["krum_rounds"]``).  The
+    per-coordinate stage is local (``ops["bulyan_stage"]``) and one all-gather
+    assembles the (d,) float64 result.
+
+    ops: bulyan_round(X, rows, nr, aggsubfunc, agg_out) -> dist (nr,) float64;
+         bulyan_pick(dist, rows, nr, rows_next); bulyan_stage(S, beta) -> (w,);
+         gram(X) -> (N, N) float64; krum_rounds(G, f, rounds) -> (rounds,) indices."""
+    n = int(X_shard.shape[0])
+    theta = n - 2 * int(f)
+    if theta <= 0:
+        # the reference indexes the empty selection (np_grads[0]): IndexError
+        raise IndexError("bulyan needs theta = N - 2f > 0 (N=%d, f=%d)" % (n, f))
+    beta = theta - 2 * int(f)
+    on = dist.is_initialized()   # (a 1-rank group still goes through the collectives)
+    if aggsubfunc == "krum":
+        G = ops["gram"](X_shard).to(torch.float64).contiguous()
+        if on:
+            dist.all_reduce(G, op=dist.ReduceOp.SUM, group=group)
+        order = ops["krum_rounds"](G, int(f), theta)
+        S = X_shard.index_select(0, order.to(torch.long)).contiguous()
+    else:
+        if aggsubfunc not in ("median", "trimmedmean"):
+            raise ValueError("aggsubfunc must be krum, median or trimmedmean")
+        S = torch.empty((theta, X_shard.shape[1]), dtype=torch.float32, device=X_shard.device)
+        rows = torch.arange(n, dtype=torch.int32, device=X_shard.device)
+        nxt = torch.empty_like(rows)
+        for t in range(theta):
+            nr = n - t
+            dvec = ops["bulyan_round"](X_shard, rows, nr, aggsubfunc, S[t])
+            if on:
+                dist.all_reduce(dvec, op=dist.ReduceOp.SUM, group=group)
+            ops["bulyan_pick"](dvec, rows, nr, nxt)
+            rows, nxt = nxt, rows
+    return gather_columns(ops["bulyan_stage"](S, beta), d, align, group)
 
 
 # ---------------------------------------------------------------------------
@@ -121,14 +170,15 @@ def pipelined_coordinatewise(local_fn, X_local, d, block, group=None, out=None, 
     (RCCL over xGMI), ordered after the block's aggregation by an event; the
     aggregation of the next block proceeds concurrently on the current stream.
     Returns the (d,) aggregate on every rank."""
-    world, rank = _world(group) if dist.is_initialized() else (1, 0)
+    world, rank = _world(group)
+    on = dist.is_initialized()
     rounds = cyclic_rounds(d, world, block)
     span = world * block
     full = out
     if full is None or full.numel() < rounds * span:
         full = torch.empty(rounds * span, dtype=_out_dtype(local_fn, X_local), device=X_local.device)
     mine = cyclic_blocks(d, world, rank, block)
-    cuda = X_local.is_cuda and world > 1
+    cuda = X_local.is_cuda and on
     compute = torch.cuda.current_stream(X_local.device) if cuda else None
     if cuda and comm_stream is None:
         comm_stream = torch.cuda.Stream(device=X_local.device)
@@ -139,7 +189,7 @@ def pipelined_coordinatewise(local_fn, X_local, d, block, group=None, out=None, 
             lo, hi = mine[k]
             local_fn(X_local[:, off:off + hi - lo], seg[:hi - lo])
             off += hi - lo
-        if world == 1:
+        if not on:
             continue
         if cuda:
             ev = torch.cuda.Event()
@@ -170,7 +220,20 @@ def engine_ops():
         order, _ = engine.krum_from_gram(G, f, 1)
         return int(order[0].item())
 
+    def bulyan_round(X, rows, nr, aggsubfunc, agg):
+        dvec = torch.empty(nr, dtype=torch.float64, device=X.device)
+        engine.bulyan_round(X, rows, nr, aggsubfunc, agg, dvec)
+        return dvec
+
+    def krum_rounds(G, f, rounds):
+        order, _ = engine.krum_from_gram(G, f, rounds, scores=False)
+        return order
+
     return {
+        "bulyan_round": bulyan_round,
+        "bulyan_pick": lambda dvec, rows, nr, nxt: engine.bulyan_pick(dvec, rows, nr, nxt),
+        "bulyan_stage": lambda S, beta: engine.bulyan_stage(S, beta),
+        "krum_rounds": krum_rounds,
         "average": lambda X: engine.average(X),
         "median": lambda X: engine.median(X),
         "trimmedmean": lambda X: engine.trimmed_mean(X, 0.1),

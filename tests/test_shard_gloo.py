@@ -42,6 +42,53 @@ def _centred_gram(x):
     return z @ z.T
 
 
+def cpu_bulyan_ops():
+    """The Bulyan per-shard operations restated on CPU tensors with the oracle
+    (the GPU ranks use shard.engine_ops())."""
+    import warnings
+    from oracle import robust_np as orc
+
+    def bulyan_round(X, rows, nr, aggsubfunc, agg):
+        sub = X.numpy()[rows[:nr].numpy()]
+        a = orc.trimmed_mean(list(sub)) if aggsubfunc == "trimmedmean" else orc.median(list(sub))
+        a = np.asarray(a, dtype=np.float32)
+        agg.copy_(torch.from_numpy(a))
+        return torch.from_numpy(((sub.astype(np.float64) - a.astype(np.float64)) ** 2).sum(axis=1))
+
+    def bulyan_pick(dvec, rows, nr, nxt):
+        dv = dvec.numpy()
+        best, bv = -1, np.inf
+        for r in range(nr):
+            if dv[r] < bv:
+                best, bv = r, dv[r]
+        keep = [rows[r].item() for r in range(nr) if r != max(best, 0)]
+        nxt[:nr - 1] = torch.tensor(keep, dtype=torch.int32)
+
+    def bulyan_stage(S, beta):
+        A = S.numpy().astype(np.float64)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            return torch.from_numpy(np.array([orc.bulyan_one_coordinate_leftfirst(A[:, j], beta)
+                                              for j in range(A.shape[1])]))
+
+    def krum_rounds(G, f, rounds):
+        g = G.numpy()
+        sq = np.diag(g)[:, None] + np.diag(g)[None, :] - 2 * g
+        dd = np.sqrt(np.maximum(sq, 0)).astype(np.float32)
+        alive, order = list(range(g.shape[0])), []
+        for _ in range(rounds):
+            sc = orc.krum_scores_from_dist(dd[np.ix_(alive, alive)], f)
+            i = int(np.argmin(sc))
+            order.append(alive.pop(i))
+        return torch.tensor(order, dtype=torch.int32)
+
+    return {"bulyan_round": bulyan_round, "bulyan_pick": bulyan_pick, "bulyan_stage": bulyan_stage,
+            "gram": lambda X: torch.from_numpy(_centred_gram(X.numpy())), "krum_rounds": krum_rounds}
+
+
+BULYAN_CASE = dict(n=30, d=257, f=5, seed=14, byz=5)
+
+
 def _worker(rank, world, port, results):
     _setup_paths()
     from srfl_amd import shard
@@ -93,6 +140,14 @@ def _worker(rank, world, port, results):
             def tm_into(X, o):
                 o.copy_(torch.from_numpy(np.asarray(orc.trimmed_mean(list(X.numpy())))))
             out["cyclic_%d" % block] = shard.pipelined_coordinatewise(tm_into, Xc, d, block).numpy().copy()
+        # Bulyan: per-round all-reduce of the distance partials (median /
+        # trimmed mean), all-reduced Gram (krum), local per-coordinate stage
+        c = BULYAN_CASE
+        xb = make_rows(c["n"], c["d"], seed=c["seed"], byz=c["byz"])
+        lo, hi = shard.shard_bounds(c["d"], world, rank)
+        Xb = torch.from_numpy(np.ascontiguousarray(xb[:, lo:hi]))
+        for mode in ("krum", "median", "trimmedmean"):
+            out["bulyan_" + mode] = shard.bulyan(cpu_bulyan_ops(), Xb, c["d"], c["f"], mode).numpy()
         results[rank] = out
     finally:
         dist.destroy_process_group()
@@ -191,3 +246,36 @@ def test_sharded_krum_equals_unsharded(two_rank_results):
     for r in (0, 1):
         assert two_rank_results[r]["krum_idx"] == idx
         np.testing.assert_array_equal(two_rank_results[r]["krum_row"], row)
+
+
+@pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
+def test_sharded_bulyan_equals_unsharded(mode, two_rank_results, three_rank_results):
+    """Same selection and the same per-coordinate results with 2 and 3 column
+    shards as unsharded (world 1, no process group), and the reference-equivalent
+    oracle within fp64 rounding."""
+    _setup_paths()
+    import warnings
+    from srfl_amd import shard
+    from oracle import robust_np as orc
+    from synth import make_rows
+    c = BULYAN_CASE
+    xb = make_rows(c["n"], c["d"], seed=c["seed"], byz=c["byz"])
+    want = shard.bulyan(cpu_bulyan_ops(), torch.from_numpy(xb), c["d"], c["f"], mode).numpy()
+    for res in (two_rank_results, three_rank_results):
+        for r in res:
+            np.testing.assert_array_equal(res[r]["bulyan_" + mode], want)
+    rows = [r for r in xb]
+    sel, _ = orc.bulyan_select(rows, c["f"], mode)
+    S = np.array([np.asarray(g, dtype=np.float64).ravel() for g in sel])
+    beta = S.shape[0] - 2 * c["f"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ref = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j], beta) for j in range(S.shape[1])])
+    np.testing.assert_allclose(want, ref, rtol=1e-12, atol=1e-15)
+
+
+def test_sharded_bulyan_theta_error():
+    _setup_paths()
+    from srfl_amd import shard
+    with pytest.raises(IndexError):
+        shard.bulyan(cpu_bulyan_ops(), torch.zeros(10, 4), 4, 5, "median")
