@@ -280,6 +280,20 @@ def main():
     out = torch.empty(d, dtype=odt, device=device)
     full = torch.empty(d * world, dtype=odt, device=device) if world > 1 else None
     fn = AGG[a.agg]
+    # N>1, Krum / Bulyan: the selection is global -- the sharded forms exchange
+    # the N x N Gram (one all-reduce) or, per Bulyan round, the <= N distance
+    # partials (one all-reduce each), then assemble the (d*world,) result
+    sharded = None
+    if world > 1 and a.agg in ("krum", "mom_krum", "bulyankrum", "bulyanmedian", "bulyantrimmedmean"):
+        ops = shard.engine_ops()
+        dtot = d * world
+        if a.agg == "krum":
+            sharded = lambda: shard.krum(ops["gram"], ops["krum_select"], X, dtot, 20)[0]
+        elif a.agg == "mom_krum":
+            nb = -(-n // 3)
+            sharded = lambda: shard.krum(ops["gram"], ops["krum_select"], engine.bucket_means(X, 3, nb), dtot, 20)[0]
+        else:
+            sharded = lambda: shard.bulyan(ops, X, dtot, 20, a.agg[len("bulyan"):])
     # N>1, coordinate-wise: block-cyclic shard (this rank's X = its blocks side
     # by side) with the in-place all-gather of block k on a second stream,
     # overlapped with the k-select of block k+1 (srfl_amd/shard.py)
@@ -293,10 +307,13 @@ def main():
             return
         if ev is not None:
             ev[0].record()
-        fn(X, out)
+        if sharded is not None:
+            full.copy_(sharded())
+        else:
+            fn(X, out)
         if ev is not None:
             ev[1].record()
-        if world > 1:
+        if world > 1 and sharded is None:
             dist.all_gather_into_tensor(full, out)
 
     for _ in range(a.warmup):
@@ -358,7 +375,9 @@ def main():
                        a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
                    "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, a.chunks)
-                                   if pipelined else "d-shard x%d" % world)},
+                                   if pipelined else
+                                   ("d-shard x%d, all-reduced selection" % world if sharded is not None
+                                    else "d-shard x%d" % world))},
         "roofline": {"bound": bound, "kernel": kernel_label(a.agg, n), "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": traffic, "kernel_ms": round(kern_ms, 4),
