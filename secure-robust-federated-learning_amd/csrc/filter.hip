@@ -41,6 +41,8 @@
 //   chunk_mean_kernel   mu_j = sum_i c_i x_ij / sum_i c_i in fp64 over the kept
 //                       clients in client order (the reference's np.average),
 //                       one lane per coordinate; HBM bound.
+#include <type_traits>
+
 #include "sra_common.hpp"
 
 namespace sra {
@@ -372,6 +374,9 @@ struct SolveArgs {
   double sigma;
   double expansion;
   double* dbg;       // optional diagnostics of the batch's chunk 0
+  double* Vg;        // lanczos_solve_kernel: [grid][MMAX][FNP] Lanczos basis per workgroup
+  int* fb_list;      // chunks handed to the re-orthogonalising fallback
+  int* fb_count;
 };
 
 constexpr size_t kSolveLds =
@@ -624,7 +629,10 @@ __device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int
   return ok;
 }
 
-template <int MODE, bool DBG>  // MODE 0: filterL2, 1: ex_noregret; DBG: diagnostics of chunk 0
+// MODE 0: filterL2, 1: ex_noregret; DBG: diagnostics of chunk 0.  Since round
+// 2 this re-orthogonalising solver is the fallback: it runs only the chunks
+// that lanczos_solve_kernel listed in A.fb_list (A.fb_count on the device).
+template <int MODE, bool DBG>
 __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* V = reinterpret_cast<double*>(smem);   // [LMAX][VST] Lanczos basis
@@ -699,7 +707,9 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
     return bi;
   };
 
-  for (int ch = blockIdx.x; ch < A.nb; ch += gridDim.x) {
+  const int nlisted = *A.fb_count;
+  for (int li = blockIdx.x; li < nlisted; li += gridDim.x) {
+    const int ch = A.fb_list[li];
     // ---- G rows into registers: lane pair (row, half) holds G[row][64 half + c]
     double g[64];
     {
@@ -1024,6 +1034,610 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
 }
 
 // ============================================================================
+// lanczos_solve_kernel: the filter iterations with plain Lanczos
+// ============================================================================
+// Each iteration's top eigenvector is essentially new (the filter just damped
+// the previous top direction: consecutive eigenvectors overlap ~0.1 on the
+// bench data), so every iteration runs ~50-90 Lanczos steps from scratch.
+// Plain three-term Lanczos stopped within a few steps of convergence gives the
+// top Ritz pair to ~3e-15 (modelled in numpy against LAPACK; Paige: the loss
+// of orthogonality only sets in along a Ritz vector once it has converged),
+// so this solver keeps no basis on chip and does no re-orthogonalisation:
+// two block reductions per step (alpha; |r|^2 with the centring sums of the
+// next vector), the basis vectors go to a per-workgroup global scratch (L2)
+// for the Ritz vector, and the LDS per chunk drops from 80 KiB to ~22 KiB.
+// Checks run at most kMaxAdvance steps apart once a first check has measured
+// the residual decay, so a check never lands after a ghost copy of the top
+// Ritz value has formed (~15-20 steps after convergence).  A chunk that has
+// not converged after MMAX steps, or whose residual grows between checks (a
+// ghost), is listed for filter_solve_kernel and redone from its first iteration.
+constexpr int MMAX = 128;          // plain Lanczos steps per eigenproblem (two lane slots of the check)
+constexpr int TW = 2 * MMAX + 4;   // per-wave T record: (alpha_q, beta^2_{q-1}) interleaved, then z
+constexpr int kMaxAdvance = 8;     // checks at most this far apart (a ghost forms ~15-20 steps past convergence)
+constexpr double kAccept = 2.5e-16;  // plain Lanczos: accept the Ritz pair at residual <= kAccept * lambda
+
+__device__ __forceinline__ double rl_any(const double (&v)[2], int q) {
+  // q wave-uniform: both readlanes land in SGPRs, the select is scalar
+  const double a = readlane_f64(v[0], q & 63), b = readlane_f64(v[1], q & 63);
+  return q < 64 ? a : b;
+}
+
+// Top Ritz pair of T_m (m <= MMAX), block-wide (all four waves call it):
+//   1. its eigenvalue by multisection on Sturm counts over 256 points (64 per
+//      wave; the division-free recurrence P_k = (alpha_k - x) P_{k-1} -
+//      beta^2 P_{k-2} with (alpha, beta^2) pairs broadcast from LDS, one
+//      barrier per round).  theta_lb (the previous check's Ritz value, a lower
+//      bound by interlacing) and hint (its last increase) give a first bracket
+//      a few ulps to a few 1e-10 wide; without them the first round is
+//      geometric above max(alpha_0, theta_lb);
+//   2. the forward pivots dp_q on wave 0 and the backward pivots dm_q on wave 1
+//      at the same time (serial chains on register-resident T, readlane);
+//   3. wave 0: the twist (smallest |gamma_q|), the product walks, the
+//      normalised eigenvector into z[0, m).
+// Record layout: T[2q] = alpha_q, T[2q+1] = beta^2 of (q-1, q).  The residual
+// of the pair is beta_m |z_{m-1}| (returned in *zlast_out): the last component
+// must come from the twisted factorisation -- P_{m-1}(theta) / P_m'(theta)
+// has a ~1e-16 floor once consecutive Ritz values agree to the last ulp.
+// scr: >= 2 * MMAX + 16 doubles of LDS.
+__device__ __attribute__((noinline)) void block_check(const double* T, int m, double theta_lb, double hint,
+                                                      double tscale, double* z, double* scr, double* theta_out,
+                                                      double* zlast_out, int* rounds_out) {
+  m = __builtin_amdgcn_readfirstlane(m);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double2* T2 = reinterpret_cast<const double2*>(T);
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(scr + 2 * MMAX);   // [2][4]
+  double* res = scr + 2 * MMAX + 8;                                                    // [4] results
+  // Gershgorin bounds (every wave, identical)
+  double glo = 1e300, ghi = -1e300;
+  for (int q = lane; q < m; q += 64) {
+    const double r = (q >= 1 ? sqrt(T[2 * q + 1]) : 0.0) + (q + 1 < m ? sqrt(T[2 * q + 3]) : 0.0);
+    glo = fmin(glo, T[2 * q] - r);
+    ghi = fmax(ghi, T[2 * q] + r);
+  }
+  glo = wave_min(glo);
+  ghi = wave_max(ghi);
+  const double a0 = T[0];
+  double lo = fmax(glo, fmax(theta_lb, a0));
+  double hi = ghi;
+  if (!(lo < hi)) lo = glo;
+  const bool hinted = hint >= 0.0 && theta_lb > -1e299;
+  const double hg = lo + 4.0 * hint + 4e-16 * fabs(lo);
+  auto count = [&](double x) -> int {
+    double p2 = 1.0, p1 = a0 - x;
+    unsigned cnt = static_cast<unsigned>(__builtin_bit_cast(unsigned long long, p1) >> 63);
+    auto step = [&](double2 t) __attribute__((always_inline)) {
+      const double pk = fma(t.x - x, p1, -(t.y * p2));
+      cnt += static_cast<unsigned>((__builtin_bit_cast(unsigned long long, pk) ^
+                                    __builtin_bit_cast(unsigned long long, p1)) >> 63);
+      p2 = p1;
+      p1 = pk;
+    };
+    int q = 1;
+    for (; q + 4 <= m; q += 4) {
+      const double2 t0 = T2[q], t1 = T2[q + 1], t2 = T2[q + 2], t3 = T2[q + 3];
+      step(t0);
+      step(t1);
+      step(t2);
+      step(t3);
+      const int e = __builtin_amdgcn_frexp_exp(p1);
+      p1 = __builtin_amdgcn_ldexp(p1, -e);
+      p2 = __builtin_amdgcn_ldexp(p2, -e);
+    }
+    for (; q < m; ++q) step(T2[q]);
+    return static_cast<int>(cnt);
+  };
+  int round = 0;
+  for (; round < 24; ++round) {
+    // point p of this round (identical formula in every lane)
+    const int kind = round == 0 ? (hinted && hg < hi ? 1 : 2) : 0;
+    const double rlo = lo, rhi = hi;
+    auto point = [&](int p) -> double {
+      if (kind == 1) return p < 255 ? rlo + (hg - rlo) * ((p + 1) * (1.0 / 255.0)) : rhi;
+      if (kind == 2) return rlo + (rhi - rlo) * __builtin_amdgcn_ldexp(1.0, p - 255);
+      return rlo + (rhi - rlo) * ((p + 1) * (1.0 / 257.0));
+    };
+    const unsigned long long ok = __builtin_amdgcn_ballot_w64(count(point(64 * wave + lane)) >= m);
+    unsigned long long* M = masks + 4 * (round & 1);
+    if (lane == 0) M[wave] = ok;
+    __syncthreads();
+    int first = 256;
+    for (int w = 3; w >= 0; --w)
+      if (M[w]) first = 64 * w + __builtin_ctzll(M[w]);
+    const double xf = first < 256 ? point(first) : rhi;
+    const double xb = first > 0 ? point(first - 1) : rlo;
+    const bool stalled = xb == lo && xf == hi;
+    lo = xb;
+    hi = xf;
+    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
+  }
+  const double lm = 0.5 * (lo + hi);
+  // ---- pivots: forward on wave 0, backward on wave 1
+  const double tiny = 1e-300 + 1e-30 * tscale;
+  double al[2], b2[2], bl[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int q = lane + 64 * s;
+    al[s] = q < m ? T[2 * q] : 0.0;
+    b2[s] = q + 1 < m ? T[2 * q + 3] : 0.0;
+    bl[s] = sqrt(b2[s]);
+  }
+  double* dps = scr;          // [MMAX] forward pivots
+  double* dms = scr + MMAX;   // [MMAX] backward pivots
+  const int e0 = m < 64 ? m : 64;
+  if (wave == 0) {
+    double dp[2] = {0.0, 0.0};
+    double pf = 0.0;
+    auto fwd = [&](auto S, int q) __attribute__((always_inline)) {
+      constexpr int s = decltype(S)::value;
+      double v = readlane_f64(al[s], q & 63) - lm;
+      if (q > 0) v -= fdiv(s == 0 || q > 64 ? readlane_f64(b2[s], (q - 1) & 63) : readlane_f64(b2[0], 63), pf);
+      if (fabs(v) < tiny) v = -tiny;
+      pf = v;
+      dp[s] = lane == (q & 63) ? v : dp[s];
+    };
+    for (int q = 0; q < e0; ++q) fwd(std::integral_constant<int, 0>{}, q);
+    for (int q = 64; q < m; ++q) fwd(std::integral_constant<int, 1>{}, q);
+    dps[lane] = dp[0];
+    dps[lane + 64] = dp[1];
+  } else if (wave == 1) {
+    double dm[2] = {0.0, 0.0};
+    double pb = 0.0;
+    auto bwd = [&](auto S, int q) __attribute__((always_inline)) {
+      constexpr int s = decltype(S)::value;
+      double v = readlane_f64(al[s], q & 63) - lm;
+      if (q < m - 1) v -= fdiv(readlane_f64(b2[s], q & 63), pb);
+      if (fabs(v) < tiny) v = -tiny;
+      pb = v;
+      dm[s] = lane == (q & 63) ? v : dm[s];
+    };
+    for (int q = m - 1; q >= 64; --q) bwd(std::integral_constant<int, 1>{}, q);
+    for (int q = e0 - 1; q >= 0; --q) bwd(std::integral_constant<int, 0>{}, q);
+    dms[lane] = dm[0];
+    dms[lane + 64] = dm[1];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const double dp[2] = {dps[lane], dps[lane + 64]};
+    const double dm[2] = {dms[lane], dms[lane + 64]};
+    const double dmn[2] = {dms[lane + 1], lane + 65 < MMAX ? dms[lane + 65] : 0.0};
+    double gam = 1e308;
+    int tw = 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = lane + 64 * s;
+      const double gq = q < m ? fabs(dp[s] + dm[s] - (al[s] - lm)) : 1e308;
+      if (gq < gam) {
+        gam = gq;
+        tw = q;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double og = __shfl_xor(gam, off);
+      const int ot = __shfl_xor(tw, off);
+      if (og < gam || (og == gam && ot < tw)) {
+        gam = og;
+        tw = ot;
+      }
+    }
+    tw = __builtin_amdgcn_readfirstlane(tw);
+    // q < tw: z_q = -(b_q / dp_q) z_{q+1};  q >= tw: z_{q+1} = -(b_q / dm_{q+1}) z_q
+    double rat[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = lane + 64 * s;
+      rat[s] = q < tw ? -bl[s] / dp[s] : (q + 1 < m ? -bl[s] / dmn[s] : 0.0);
+    }
+    double zv[2] = {lane == tw ? 1.0 : 0.0, lane + 64 == tw ? 1.0 : 0.0};
+    {
+      double zd = 1.0, zu = 1.0;
+      const int sd = tw, su = m - 1 - tw;
+      const int steps = sd > su ? sd : su;
+      for (int k = 0; k < steps; ++k) {
+        if (k < sd) {
+          const int q = tw - 1 - k;
+          zd *= rl_any(rat, q);
+          if (fabs(zd) > 1e150) zd = copysign(1e150, zd);
+          if (q < 64) zv[0] = lane == q ? zd : zv[0];
+          else zv[1] = lane == q - 64 ? zd : zv[1];
+        }
+        if (k < su) {
+          const int q = tw + k;
+          zu *= rl_any(rat, q);
+          if (fabs(zu) > 1e150) zu = copysign(1e150, zu);
+          if (q + 1 < 64) zv[0] = lane == q + 1 ? zu : zv[0];
+          else zv[1] = lane == q + 1 - 64 ? zu : zv[1];
+        }
+      }
+    }
+    const double amax = wave_max(fmax(fabs(zv[0]), fabs(zv[1])));
+    const double zs0 = zv[0] / amax, zs1 = zv[1] / amax;
+    const double inv = 1.0 / sqrt(wave_sum(zs0 * zs0 + zs1 * zs1));
+    if (lane < m) z[lane] = zs0 * inv;
+    if (lane + 64 < m) z[lane + 64] = zs1 * inv;
+    const double zl = rl_any(zv, m - 1) / amax * inv;
+    if (lane == 0) {
+      res[0] = lm;
+      res[1] = zl;
+    }
+  }
+  __syncthreads();
+  *theta_out = res[0];
+  *zlast_out = res[1];
+  *rounds_out = round + 1;
+}
+
+constexpr size_t kLanczosLds =
+    sizeof(double) * (XLEN + 2 * XLEN + 32 + TW + 2 * MMAX + (2 * MMAX + 16) + 64 + 4 * FNP + 240) +
+    sizeof(int) * (3 * FNP + 16);
+
+template <int MODE, bool DBG>
+__global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* xbuf = reinterpret_cast<double*>(smem);   // [XLEN] operator input
+  double* gbuf = xbuf + XLEN;                       // [XLEN] g = G w (forming M)
+  double* sbuf = gbuf + XLEN;                       // [XLEN] sqrt(w)
+  double* red = sbuf + XLEN;                        // [2][16] block reductions (parity slots)
+  double* trw = red + 32;                           // [TW] tridiagonal record (wave 0 runs the checks)
+  double* zbuf = trw + TW;                          // [2][MMAX] eigenvectors of T (current / best check)
+  double* cscr = zbuf + 2 * MMAX;                   // [2 MMAX + 16] check scratch (pivots, masks, result)
+  double* hbuf = cscr + 2 * MMAX + 16;              // [64] projection scalar
+  double* cvec = hbuf + 64;                         // [FNP] weights (projection / final scale)
+  double* vscr = cvec + FNP;                        // [3][FNP] projection scratch
+  double* clog = vscr + 3 * FNP;                    // [60][4] DBG: check log of the current iteration
+  int* ibuf = reinterpret_cast<int*>(clog + 240);   // [3][FNP] int scratch + [16] argmax slots
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int row = tid >> 1;
+  const int half = tid & 1;
+  const bool own = half == 0;
+  const int n = A.n;
+  const int xi = row < 64 ? row : XOFF + row - 64;
+  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * MMAX * FNP;
+
+  int rslot = 0;
+  auto reduce4 = [&](double v0, double v1, double (&o)[4], int nv) __attribute__((always_inline)) {
+    v0 = wave_sum(v0);
+    if (nv > 1) v1 = wave_sum(v1);
+    double* R = red + 16 * rslot;
+    if (lane == 0) {
+      R[4 * wave + 0] = v0;
+      if (nv > 1) R[4 * wave + 1] = v1;
+    }
+    __syncthreads();
+    o[0] = (R[0] + R[4]) + (R[8] + R[12]);
+    if (nv > 1) o[1] = (R[1] + R[5]) + (R[9] + R[13]);
+    rslot ^= 1;
+  };
+  auto argmax_first = [&](double v, int i, double* vbest) __attribute__((always_inline)) -> int {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ov = __shfl_xor(v, off);
+      const int oi = __shfl_xor(i, off);
+      if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+      }
+    }
+    double* R = red + 16 * rslot;
+    int* I = ibuf + 3 * FNP + 8 * rslot;
+    if (lane == 0) {
+      R[wave] = v;
+      I[wave] = i;
+    }
+    __syncthreads();
+    double bv = R[0];
+    int bi = I[0];
+    for (int q = 1; q < 4; ++q)
+      if (R[q] > bv || (R[q] == bv && I[q] < bi)) {
+        bv = R[q];
+        bi = I[q];
+      }
+    rslot ^= 1;
+    *vbest = bv;
+    return bi;
+  };
+
+  for (int ch = blockIdx.x; ch < A.nb; ch += gridDim.x) {
+    const double2* Gr = reinterpret_cast<const double2*>(A.G + static_cast<size_t>(ch) * FNP * FNP + row * FNP +
+                                                         64 * half);
+    double g[64];   // G's row segment at the start of an iteration, then M's
+    // y = (this register matrix) x for x in xbuf; both lanes of the pair get the row value
+    auto gmv = [&]() __attribute__((always_inline)) -> double {
+      const double2* xh = reinterpret_cast<const double2*>(xbuf + XOFF * half);
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+      for (int c = 0; c < 32; c += 2) {
+        const double2 a = xh[c], b = xh[c + 1];
+        p0 = fma(g[2 * c], a.x, p0);
+        p1 = fma(g[2 * c + 1], a.y, p1);
+        p2 = fma(g[2 * c + 2], b.x, p2);
+        p3 = fma(g[2 * c + 3], b.y, p3);
+        if ((c & 6) == 6) asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)::"memory");
+      }
+      const double p = (p0 + p1) + (p2 + p3);
+      return p + dpp_f64<0xB1>(p);
+    };
+
+    const bool dbg = DBG && ch == 0;
+    bool ai;
+    if constexpr (MODE == 1) ai = A.act[static_cast<size_t>(ch) * FNP + row] != 0;
+    else ai = row < n;
+    double ci = ai ? 1.0 : 0.0;
+    const int fdrop = static_cast<int>(ceil(A.eps * n));
+    const int n_keep = MODE == 1 ? n - (fdrop < n ? fdrop : n) : n;
+    const double step = MODE == 1 ? A.misc[static_cast<size_t>(ch) * kMisc + 1] : 0.0;
+    const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n) : static_cast<int>(2 * A.eps * n_keep);
+    int m_hint = 24;
+    double rate_hint = 0.0;
+    bool fallback = false;
+    int clog_n = 0;   // DBG: checks logged (per chunk, last 60 kept from the start)
+
+    for (int it = 0; it < iters; ++it) {
+      const long long t_it = dbg ? clock64() : 0;
+      if (DBG) clog_n = 0;
+      // ---- G back into registers; weights, g = G w, s = w^T G w
+#pragma unroll
+      for (int c = 0; c < 32; ++c) {
+        const double2 v = Gr[c];
+        g[2 * c] = v.x;
+        g[2 * c + 1] = v.y;
+      }
+      double o[4];
+      reduce4(own && ai ? ci : 0.0, own && ai ? 1.0 : 0.0, o, 2);
+      const double csum = o[0];
+      const int nact = static_cast<int>(o[1]);
+      const double wi = ai ? ci / csum : 0.0;
+      const double swi = sqrt(wi > 0.0 ? wi : 0.0);
+      if (own) {
+        xbuf[xi] = wi;
+        sbuf[xi] = swi;
+      }
+      __syncthreads();
+      const double gwi = gmv();
+      if (own) gbuf[xi] = gwi;
+      reduce4(own ? wi * gwi : 0.0, 0.0, o, 1);
+      const double sgw = o[0];
+      // ---- M = W^1/2 (G - g 1^T - 1 g^T + s 1 1^T) W^1/2 in place (the Gram of
+      // sqrt(w_i) (x_i - mu): its nonzero spectrum is the weighted covariance's)
+      {
+        const double2* gh = reinterpret_cast<const double2*>(gbuf + XOFF * half);
+        const double2* sh = reinterpret_cast<const double2*>(sbuf + XOFF * half);
+        const double ri = sgw - gwi;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          const double2 gj = gh[c], sj = sh[c];
+          g[2 * c] = swi * ((g[2 * c] + ri - gj.x) * sj.x);
+          g[2 * c + 1] = swi * ((g[2 * c + 1] + ri - gj.y) * sj.y);
+        }
+      }
+
+      // ---- top eigenpair of M by plain Lanczos.  The computed residual of the
+      // top Ritz pair falls to a floor of ~1e-16 lambda and grows again once a
+      // ghost copy forms, so the best check so far is kept and accepted when
+      // the residual stalls at the floor; near convergence every step is
+      // checked.  A ghost before an acceptable residual restarts the
+      // eigenproblem once with dense checks.
+      double lam = 0.0, resid = 0.0, ui = 0.0;
+      int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
+      bool converged = false;
+      double tscale = 0.0;
+      long long tcheck = 0, tmult = 0, tvec = 0;   // diagnostics: cycles in checks
+      int trounds = 0;
+      for (int attempt = 0; attempt < 2 && !converged; ++attempt) {
+        double rt;
+        {
+          const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
+          rt = swi > 0.0 ? swi * hh : 0.0;
+        }
+        if (own) xbuf[xi] = rt;
+        reduce4(own ? rt * rt : 0.0, 0.0, o, 1);
+        double nrm2 = o[0];
+        double qprev = 0.0, theta_lb = -1e300, hint = -1.0;
+        double res_best = 1e300, lam_best = 0.0;
+        int m_best = 0;
+        tscale = 0.0;
+        // the retry samples the residual every step from the check before the
+        // first attempt's best one (the sequence is the same: only the sampling differs)
+        const int adv_max = attempt == 0 ? kMaxAdvance : 1;
+        int next_check = attempt == 0 ? (m_hint - 8 > 4 ? m_hint - 8 : 4) : (m_retry > 4 ? m_retry : 4);
+        int m_a = -1, m_last = 4, m_pre = 4;
+        double res_a = 0.0;
+        bool ghost = false;
+        for (int j = 0;; ++j) {
+          const double bet = sqrt(nrm2);
+          if (j > 0) {
+            if (tid == 0) trw[2 * j + 1] = nrm2;
+            tscale = fmax(tscale, bet);
+            const bool breakdown = !(bet > 1e-14 * tscale);
+            if (breakdown || j == MMAX || j >= next_check) {
+              const int m = j;
+              ++nchecks;
+              // top Ritz pair of T_m, block-wide (the record was written by
+              // thread 0: the barriers since order it for the other waves)
+              const long long tc0 = dbg ? clock64() : 0;
+              double lm, zl;
+              int rounds = 0;
+              block_check(trw, m, theta_lb, hint, tscale, zbuf + zcur * MMAX, cscr, &lm, &zl, &rounds);
+              if (dbg) {
+                tcheck += clock64() - tc0;
+                trounds += rounds;
+              }
+              const double res = fabs(bet * zl);
+              if (DBG && tid == 0 && clog_n < 60) {
+                double* lg = clog + 4 * clog_n;
+                lg[0] = m + 1000.0 * attempt + 10000.0 * it;
+                lg[1] = lm;
+                lg[2] = zl;
+                lg[3] = bet;
+              }
+              ++clog_n;
+              hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
+              theta_lb = lm;
+              if (res <= kAccept * fabs(lm) || breakdown) {
+                converged = true;
+                m_conv = m;
+                lam = lm;
+                resid = res;
+                zbest = zcur;
+                break;
+              }
+              const bool better = res < res_best;
+              if (better) {
+                m_pre = m_last;
+                res_best = res;
+                lam_best = lm;
+                m_best = m;
+                zbest = zcur;
+                zcur ^= 1;
+              }
+              // past the floor: the residual grows again after it was small (a
+              // ghost copy is forming; a bump during slow convergence is not one)
+              ghost = res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
+              const bool out_of_steps = j == MMAX;
+              if (ghost || out_of_steps) {
+                // the first attempt sampled the residual every few steps: the
+                // retry samples every step from the check before the best one
+                if (tid == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
+                m_retry = m_pre;
+                break;
+              }
+              int adv = 4;
+              double rate = rate_hint;
+              if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
+              if (rate < 0.0 && res > 0.0) {
+                // straight to the predicted step of the floor (kAccept)
+                const double need = log(kAccept * fabs(lm) / res) / rate;
+                adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
+              }
+              m_a = m;
+              res_a = res;
+              m_last = m;
+              next_check = m + adv;
+            }
+          }
+          // y = M r~ (r~ = beta q_j in xbuf), alpha_j = q_j . M q_j
+          const double y = gmv();
+          const double ib = 1.0 / bet;
+          const double q = rt * ib;
+          if (own) Vb[j * FNP + row] = q;
+          const double mq = y * ib;
+          reduce4(own ? q * mq : 0.0, 0.0, o, 1);
+          const double aj = o[0];
+          const double r = mq - aj * q - (j > 0 ? bet * qprev : 0.0);
+          if (tid == 0) trw[2 * j] = aj;
+          tscale = fmax(tscale, fabs(aj));
+          qprev = q;
+          rt = r;
+          if (own) xbuf[xi] = r;
+          reduce4(own ? r * r : 0.0, 0.0, o, 1);
+          nrm2 = o[0];
+        }
+        if (!ghost) break;   // out of steps without an acceptable residual: no retry
+      }
+      if (!converged) {
+        fallback = true;
+        break;
+      }
+      // ---- Ritz vector u = V z of the accepted check (the basis rows this lane
+      // pair's even lane wrote, ordered by the barriers since)
+      {
+        const double* zb = zbuf + zbest * MMAX;
+        double u0 = 0.0, u1 = 0.0;
+        int qq = 0;
+        for (; qq + 1 < m_conv; qq += 2) {
+          u0 = fma(zb[qq], Vb[qq * FNP + row], u0);
+          u1 = fma(zb[qq + 1], Vb[(qq + 1) * FNP + row], u1);
+        }
+        if (qq < m_conv) u0 = fma(zb[qq], Vb[qq * FNP + row], u0);
+        ui = swi > 0.0 ? u0 + u1 : 0.0;
+      }
+      m_hint = m_conv > 8 ? m_conv : 8;
+      if (dbg && it < 256) {
+        double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
+        if (own) rec[row] = ci;
+        if (tid == 0) {
+          rec[FNP] = lam;
+          rec[FNP + 1] = m_conv;
+          rec[FNP + 2] = resid;
+          rec[FNP + 3] = nchecks;
+          rec[FNP + 4] = nact;
+          rec[FNP + 5] = sgw;
+          rec[FNP + 6] = 0;
+          rec[FNP + 7] = 0;
+          rec[FNP + 8] = static_cast<double>(clock64() - t_it);
+          rec[FNP + 9] = static_cast<double>(tcheck);
+          rec[FNP + 10] = static_cast<double>(tmult);
+          rec[FNP + 11] = static_cast<double>(tvec);
+          rec[FNP + 12] = trounds;
+        }
+      }
+      // ---- early exit (robust_estimator.py:163-164 / :71-72)
+      if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
+      // ---- tau_i = ((x_i - mu).v)^2 = (C W^1/2 u)_i^2 / lambda = ((M u)_i / sqrt(w_i))^2 / lambda
+      if (own) xbuf[xi] = ui;
+      __syncthreads();
+      const double mu_i = gmv();
+      const double cu = swi > 0.0 ? mu_i / swi : 0.0;
+      const double ti = cu * cu / lam;
+      if constexpr (MODE == 0) {
+        double tmax = 0.0;
+        const int p = argmax_first(own && ai ? ti : -__builtin_inf(), row, &tmax);
+        const double cn = (ai && row != p) ? ci * (1.0 - ti / tmax) : 0.0;
+        reduce4(own ? fabs(cn) : 0.0, 0.0, o, 1);
+        ci = cn / o[0];
+        if (row == p) ai = false;
+      } else {
+        const int nk = n_keep;
+        const double cap = 1.0 / (1.0 - A.eps) / nk;
+        if (ai) ci = ci * (1.0 - step * ti);
+        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf)) {
+          if (tid == 0) *A.status = 2;
+          break;
+        }
+      }
+      __syncthreads();   // every wave's gmv reads of xbuf before the next iteration writes it
+    }
+
+    __syncthreads();
+    if (fallback) {
+      if (tid == 0) {
+        const int k = atomicAdd(A.fb_count, 1);
+        A.fb_list[k] = ch;
+        if (DBG && k == 0 && A.dbg != nullptr) {   // check log of the first listed chunk (records 250 on)
+          double* lg = A.dbg + FNP * FNP + 250 * kDbgRec;
+          for (int e = 0; e < 4 * (clog_n < 60 ? clog_n : 60); ++e) lg[e] = clog[e];
+        }
+      }
+      continue;
+    }
+    if (own) {
+      cvec[row] = ai ? ci : 0.0;
+      ibuf[2 * FNP + row] = ai ? 1 : 0;
+      A.c[static_cast<size_t>(ch) * FNP + row] = ai ? ci : 0.0;
+      A.act[static_cast<size_t>(ch) * FNP + row] = ai ? 1 : 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int q2 = 0;
+      double* kept = vscr;
+      for (int i = 0; i < n; ++i)
+        if (ibuf[2 * FNP + i]) kept[q2++] = cvec[i];
+      A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void list_all_kernel(int* list, int* count, int nb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < nb) list[i] = i;
+  if (i == 0) *count = nb;
+}
+
+// ============================================================================
 // chunk_mean_kernel: the weighted mean of every coordinate of the batch
 // ============================================================================
 __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
@@ -1047,12 +1661,15 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
 // ============================================================================
 // host side
 // ============================================================================
-constexpr size_t kChunkWsBytes = sizeof(double) * (FNP * FNP + FNP + kMisc) + sizeof(int) * FNP;
+// per chunk of a batch: G, weights, scalars, kept flags, fallback list slot
+constexpr size_t kChunkWsBytes = sizeof(double) * (FNP * FNP + FNP + kMisc) + sizeof(int) * (FNP + 1);
+constexpr int kLanczosGrid = 1024;   // workgroups of lanczos_solve_kernel (each owns a basis slot)
 
 size_t filter_workspace_bytes(int64_t d, int itv) {
   const int64_t nchunks = cdiv(d, itv);
   const int64_t b = nchunks < kBatch ? nchunks : kBatch;
-  return static_cast<size_t>(b) * kChunkWsBytes + 256;
+  const int64_t grid = b < kLanczosGrid ? b : kLanczosGrid;
+  return static_cast<size_t>(b) * kChunkWsBytes + static_cast<size_t>(grid) * MMAX * FNP * sizeof(double) + 528;
 }
 
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
@@ -1065,16 +1682,23 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   SRA_REQUIRE(ws != nullptr && ws_bytes >= filter_workspace_bytes(d, itv), SRA_ERR_WORKSPACE,
               "filter workspace too small: need %zu bytes", filter_workspace_bytes(d, itv));
   const int64_t bmax = nchunks < kBatch ? nchunks : kBatch;
+  const int lgrid_max = static_cast<int>(bmax < kLanczosGrid ? bmax : kLanczosGrid);
   char* base = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
   double* Gws = reinterpret_cast<double*>(base);
   double* cws = Gws + static_cast<size_t>(bmax) * FNP * FNP;
   double* mws = cws + static_cast<size_t>(bmax) * FNP;
-  int* aws = reinterpret_cast<int*>(mws + static_cast<size_t>(bmax) * kMisc);
+  double* Vws = mws + static_cast<size_t>(bmax) * kMisc;
+  int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(lgrid_max) * MMAX * FNP);
+  int* fbl = aws + static_cast<size_t>(bmax) * FNP;
+  int* fbc = fbl + bmax;   // [0] listed chunks, [1] ghost after the retry, [2] out of steps, [3] retries
   const void* solve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<0, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<0, false>))
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<1, false>));
   SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
+  const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
+                           : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
+  SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLds)));
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
     GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws};
@@ -1089,7 +1713,24 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("noregret_pre_kernel");
       if (rc) return rc;
     }
-    SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr};
+    SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc};
+    SRA_HIP(hipMemsetAsync(fbc, 0, 4 * sizeof(int), s));
+    const int lgrid = nb < lgrid_max ? nb : lgrid_max;
+    if (mode == 1) {
+      // ex_noregret damps the top direction gently, so its top two eigenvalues
+      // close in (gaps ~1e-3 after a few iterations) and plain Lanczos stalls
+      // above the accuracy floor in a third of the chunks: every chunk goes to
+      // the re-orthogonalising solver
+      hipLaunchKernelGGL(list_all_kernel, dim3(cdiv(nb, 256)), dim3(256), 0, s, fbl, fbc, nb);
+      rc = launch_status("list_all_kernel");
+      if (rc) return rc;
+    } else {
+      if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<0, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      else hipLaunchKernelGGL((lanczos_solve_kernel<0, false>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      rc = launch_status("lanczos_solve_kernel");
+      if (rc) return rc;
+    }
+    // the listed chunks (not converged / ghost) on the re-orthogonalising solver
     const int grid = nb < 512 ? nb : 512;
     if (mode == 0 && dbg) hipLaunchKernelGGL((filter_solve_kernel<0, true>), dim3(grid), dim3(256), kSolveLds, s, sa);
     else if (mode == 0) hipLaunchKernelGGL((filter_solve_kernel<0, false>), dim3(grid), dim3(256), kSolveLds, s, sa);
@@ -1097,6 +1738,10 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     else hipLaunchKernelGGL((filter_solve_kernel<1, false>), dim3(grid), dim3(256), kSolveLds, s, sa);
     rc = launch_status("filter_solve_kernel");
     if (rc) return rc;
+    // diagnostics: the first batch's fallback count, as an int32 in the low
+    // word of the last record's last slot
+    if (dbg != nullptr && c0 == 0)
+      SRA_HIP(hipMemcpyAsync(dbg + FNP * FNP + 255 * kDbgRec + kDbgRec - 2, fbc, 4 * sizeof(int), hipMemcpyDeviceToDevice, s));
     const int64_t jend = (c0 + nb) * static_cast<int64_t>(itv);
     const int64_t ncols = (jend < d ? jend : d) - c0 * static_cast<int64_t>(itv);
     hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws,
