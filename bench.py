@@ -136,12 +136,12 @@ KERNEL_NAME = {
     "krum": "whole krum op (bf16x3 gram_partial_kernel dominant; per-kernel split in profiles/)",
     "mom_krum": "whole mom_krum op (bucket means + bf16x3 Gram + scoring)",
     "bulyankrum": "whole bulyan op (bf16x3 Gram + theta Krum rounds + final stage)",
-    "bulyanmedian": "whole bulyan op (theta select+distance rounds + final stage)",
-    "bulyantrimmedmean": "whole bulyan op (theta select+distance rounds + final stage)",
-    "filterl2": "spectral_filter_kernel<0> (chunk Gram on fp64 MFMA + client-space solver)",
-    "ex_noregret": "spectral_filter_kernel<1> (chunk Gram on fp64 MFMA + client-space solver)",
-    "mom_filterl2": "whole op (bucket means + spectral_filter_kernel<0>)",
-    "mom_ex_noregret": "whole op (bucket means + spectral_filter_kernel<1>)",
+    "bulyanmedian": "whole bulyan op (theta fused select+distance rounds + final stage)",
+    "bulyantrimmedmean": "whole bulyan op (theta fused select+distance rounds + final stage)",
+    "filterl2": "whole filterL2 op (chunk_gram_kernel fp64 MFMA + filter_solve_kernel<0> + chunk_mean_kernel)",
+    "ex_noregret": "whole ex_noregret op (chunk Gram + noregret_pre_kernel + filter_solve_kernel<1> + chunk means)",
+    "mom_filterl2": "whole op (bucket means + chunk Gram + filter_solve_kernel<0> + chunk means)",
+    "mom_ex_noregret": "whole op (bucket means + chunk Gram + filter_solve_kernel<1> + chunk means)",
 }
 
 
@@ -182,9 +182,36 @@ def roofline_model(agg, n, d):
         theta = n - 40
         return "hbm", HBM_PEAK_GBS, "GB/s", 4 * d * sum(n - i for i in range(theta)) + 8 * theta * d + 4 * d
     if agg in ("filterl2", "ex_noregret"):
+        # chunk Grams (fp64 MFMA) + the client-space solver (fp64), the solver
+        # priced from chunk 0's measured Lanczos steps (solver_flops below)
         return "mfma", MFMA64_PEAK_TFLOPS, "TFLOP/s", n * (n + 1) * d
     # MoM filters: bucket pass (HBM) dominates at C5
     return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
+
+
+def solver_flops(agg, X, itv=1000):
+    """fp64 flops of the spectral filters' client-space solver for one call,
+    priced from chunk 0's per-iteration Lanczos step counts (engine.filter_debug,
+    outside the timed region): per iteration M = W^1/2 C W^1/2 is formed
+    (~3 n_a^2) and every Lanczos step is one symmetric matvec (2 n_a^2) plus
+    O(n_a) vector work, n_a = the clients still active.  Chunks are assumed
+    to take chunk 0's step counts (they see statistically identical data)."""
+    mode = 0 if agg == "filterl2" else 1
+    fa = FILTER_ARGS
+    Xc = X[:, :itv]
+    _, _, recs = engine.filter_debug(Xc, mode, fa["eps"], fa["sigma"], fa["expansion"], fa["itv"])
+    recs = recs.numpy()
+    per_chunk = 0.0
+    iters = 0
+    for r in recs:
+        if not np.isfinite(r[128]):
+            break
+        na = float(r[132]) if np.isfinite(r[132]) and r[132] > 0 else float(X.shape[0])
+        steps = float(r[129])
+        per_chunk += 3 * na * na + steps * (2 * na * na + 10 * na)
+        iters += 1
+    nchunks = -(-int(X.shape[1]) // itv)
+    return per_chunk * nchunks, iters
 
 
 def cpu_baseline(agg, n, budget_s):
@@ -298,12 +325,29 @@ def main():
     # by side) with the in-place all-gather of block k on a second stream,
     # overlapped with the k-select of block k+1 (srfl_amd/shard.py)
     pipelined = world > 1 and a.agg in ("trimmedmean", "median", "average") and d % a.chunks == 0
-    comm = torch.cuda.Stream(device=device) if pipelined else None
+    block = d // a.chunks if pipelined else None
     into = shard.engine_ops()[a.agg + "_into"] if pipelined else None
+    # N>1, spectral filters (config C5: mom_filterl2 at N=512): chunks of itv
+    # coordinates are independent (robust_estimator.py:116-125, 192-201), so
+    # the same block-cyclic pipeline runs with itv-aligned blocks
+    if world > 1 and a.agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
+        itv = FILTER_ARGS["itv"]
+        nblk = next((c for c in range(a.chunks, 0, -1) if d % (c * itv) == 0), 0)
+        if nblk:
+            pipelined = True
+            block = d // nblk
+            into = lambda Xc, o: o.copy_(fn_into(Xc))   # noqa: E731
+            ffn = {"filterl2": engine.filter_l2, "ex_noregret": engine.ex_noregret,
+                   "mom_filterl2": engine.mom_filter_l2, "mom_ex_noregret": engine.mom_ex_noregret}[a.agg]
+            if a.agg.startswith("mom_"):
+                fn_into = lambda Xc: ffn(Xc, delta=MOM_DELTA, check=False, **FILTER_ARGS)   # noqa: E731
+            else:
+                fn_into = lambda Xc: ffn(Xc, check=False, **FILTER_ARGS)   # noqa: E731
+    comm = torch.cuda.Stream(device=device) if pipelined else None
 
     def step(ev=None):
         if pipelined:
-            shard.pipelined_coordinatewise(into, X, d * world, d // a.chunks, out=full, comm_stream=comm)
+            shard.pipelined_coordinatewise(into, X, d * world, block, out=full, comm_stream=comm)
             return
         if ev is not None:
             ev[0].record()
@@ -347,6 +391,12 @@ def main():
     value = total_bytes / (elapsed / a.steps) / 1e9
 
     bound, peak, unit, alg = roofline_model(a.agg, n, d)
+    solver_note = None
+    if a.agg in ("filterl2", "ex_noregret"):
+        sflops, iters = solver_flops(a.agg, X)
+        alg = alg + int(sflops)
+        solver_note = "chunk Grams n(n+1)d + solver %.3g flop (chunk 0: %d iterations, its Lanczos steps)" % (
+            sflops, iters)
     scale = 1e9 if unit == "GB/s" else 1e12
     achieved = alg / (kern_ms * 1e-3) / scale
     traffic = None
@@ -374,15 +424,20 @@ def main():
         "config": {"workload": "%s N=%d clients x d=%.0e fp32 per GPU%s" % (
                        a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
-                   "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, a.chunks)
+                   "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, d // block)
                                    if pipelined else
                                    ("d-shard x%d, all-reduced selection" % world if sharded is not None
                                     else "d-shard x%d" % world))},
         "roofline": {"bound": bound, "kernel": kernel_label(a.agg, n), "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-                     "traffic": traffic, "kernel_ms": round(kern_ms, 4),
+                     "traffic": traffic,
+                     "traffic_source": ("rocprofv3 PMC of a separate run (profiles/traffic.json, tools/pmc.sh)"
+                                        if traffic is not None else None),
+                     "kernel_ms": round(kern_ms, 4),
                      ("algorithmic_bytes_per_launch" if unit == "GB/s" else "algorithmic_flops_per_launch"): alg},
     }
+    if solver_note:
+        line["roofline"]["model"] = solver_note
     if rank == 0 and world == 1 and not a.no_host:
         del X
         torch.cuda.empty_cache()

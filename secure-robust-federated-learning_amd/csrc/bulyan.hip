@@ -26,6 +26,8 @@
 //   so the reference's argmin picks index 0: the centre is then the first
 //   selected value, NaN distances sort last, and the result is NaN only when
 //   a NaN is among the kept values.
+#include <algorithm>
+
 #include "sra_common.hpp"
 
 namespace sra {
@@ -52,239 +54,216 @@ __device__ __forceinline__ float ld_lane(const char* row, unsigned off) {
   return __builtin_nontemporal_load(reinterpret_cast<gfloat*>(reinterpret_cast<uint64_t>(row) + off));
 }
 
+// One round of the median / trimmed-mean modes as ONE pass over the remaining
+// rows (robust_estimator.py:297-322).  Per 256-coordinate block tile:
+//   1. each wave loads the column of every listed row (one lane per
+//      coordinate, the row list in VGPRs, row bases broadcast by readlane) and
+//      runs the k-select network -> the round's aggregate for its 64
+//      coordinates (written out: it is the t-th selected vector);
+//   2. it then re-issues the SAME loads, row by row (the lines it has just
+//      read: L2 / Infinity Cache hits, not HBM), writes agg - x to an LDS tile
+//      of 32 rows x 64 coordinates, and reads it back transposed -- lanes
+//      l and l + 32 hold row l's two 32-coordinate halves -- so each row's
+//      squared distance over the wave's 64 coordinates is an in-order fp32
+//      fma chain per half plus one cross-half add;
+//   3. the block's four waves are added in order (fp32), into a per-block,
+//      per-row partial; bulyan_dist_reduce_kernel sums the blocks in order in
+//      fp64.  Deterministic for a given d (sharded or not: a shard's dist is
+//      its own columns' share).
+// Blocks take runs of consecutive tiles (one tile each up to d = 16.7M), so
+// the partial table is at most kRoundMaxBlocks x n floats.
+// Measured at N=128, f=20, d=1e7 (C3): 2.06 ms per P=128 round against 1.30 +
+// 0.58 ms for round 1's k-select and distance kernels; the re-read is served
+// by the Infinity Cache but still costs fabric bandwidth.
+constexpr int kRoundMaxBlocks = 65536;
+
 template <int P, int MODE>  // MODE: 0 median, 1 trimmed; n in (P-16, P] (P=16: 1..16)
-__global__ void __launch_bounds__(256) select_rows_kernel(const float* __restrict__ X, int64_t ldx,
-                                                          const int* __restrict__ rows, int n, int64_t d, int lo,
-                                                          int hi, float* __restrict__ out) {
+__global__ void __launch_bounds__(256) select_dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
+                                                               const int* __restrict__ rows, int n_arg, int64_t d,
+                                                               int lo, int hi, float* __restrict__ out,
+                                                               float* __restrict__ bpart, int nb, int tpb) {
   constexpr int P2 = next_pow2(P);
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256;
-  const int64_t rem = d - base;
   const unsigned t = threadIdx.x;
-  const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
-  const unsigned off = (t < last ? t : last) * 4u;
-  const int k_bottom = MODE == 0 ? (P - n) / 2 : 0;
+  const unsigned lane = t & 63u;
+  const unsigned w = t >> 6;
   // the row list in VGPRs (lane l holds rows[l], rows[64 + l], ...): each
   // row index is then a readlane, not a dependent scalar load per row
   constexpr int RW = (P + 63) / 64;
   int rl[RW];
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
-    const int li = 64 * q + static_cast<int>(t & 63);
-    rl[q] = rows[li < n ? li : n - 1];
+    const int li = 64 * q + static_cast<int>(lane);
+    rl[q] = rows[li < n_arg ? li : n_arg - 1];
   }
-  constexpr int kFirstPad = P > 16 ? P - 16 : 0;   // rows below this are always real (n > P - 16)
-  float v[P2];
+  __shared__ float aggs[4][64];
+  __shared__ float dl[4][32][68];   // row stride 68 words: the transposed b128 reads spread over the banks
+  __shared__ float wsum[4][P];
+  float bs = 0.f;
+  const int n_out = n_arg;
+  const int64_t ntiles = cdiv(d, 256);
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * tpb;
+  const int64_t t1 = t0 + tpb < ntiles ? t0 + tpb : ntiles;
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    const int64_t base = tile * 256;
+    const int64_t rem = d - base;
+    const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
+    const unsigned off = (t < last ? t : last) * 4u;
+    // per tile: otherwise the row bases are hoisted out of the tile loop and
+    // held (spilled) in SGPRs
 #pragma unroll
-  for (int i = 0; i < kFirstPad; ++i) {
-    // lane i % 64 of block i / 64 holds rows[i]
-    const int row = __builtin_amdgcn_readlane(rl[i / 64], i % 64);
-    const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
-    v[i] = ld_lane(rp, off);
-    __builtin_amdgcn_sched_barrier(0);
-  }
+    for (int q = 0; q < RW; ++q) asm volatile("" : "+v"(rl[q]));
+    // n per tile as well: the ~2P row-count conditions (64-bit masks) would
+    // otherwise be hoisted and spilled to VGPR lanes (a v_readlane each)
+    int n = n_arg;
+    asm volatile("" : "+s"(n));
+    const int k_bottom = MODE == 0 ? (P - n) / 2 : 0;
+    auto load = [&](int i, bool again = false) -> float {
+      int row = __builtin_amdgcn_readlane(rl[i / 64], i % 64);
+      // the second pass recomputes the row base: kept from the first pass, the
+      // 128 64-bit bases would be held in (spilled) SGPRs across the network
+      if (again) asm volatile("" : "+s"(row));
+      const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
+      // default cache policy (not nt): step 2 re-reads these lines.  A/B at
+      // N=128, d=1e7: 2.06 ms (default) vs 2.14 (nt) per P=128 round; keeping
+      // an unsorted copy in registers instead (AGPR-backed): 2.63 ms
+      return *reinterpret_cast<const float*>(rp + off);
+    };
+    constexpr int kFirstPad = P > 16 ? P - 16 : 0;   // rows below this are always real (n > P - 16)
+    float v[P2];
 #pragma unroll
-  for (int i = kFirstPad; i < P; ++i) {
-    // lane i % 64 of block i / 64 holds rows[min(i, n - 1)] (clamped above)
-    const int row = __builtin_amdgcn_readlane(rl[i / 64], i % 64);
-    const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
-    const float x = ld_lane(rp, off);
-    __builtin_amdgcn_sched_barrier(0);
-    const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
-    v[i] = i < n ? x : pad;
-  }
-  // NaN detection over all slots (pads are +-inf, never NaN)
-  float m = v[0];
-#pragma unroll
-  for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, v[i]);
-  int nan_cnt = 0;
-  if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const bool isn = __builtin_isnan(v[i]);
-      nan_cnt += isn ? 1 : 0;
-      v[i] = isn ? __builtin_inff() : v[i];
+    for (int i = 0; i < kFirstPad; ++i) {
+      v[i] = load(i);
+      __builtin_amdgcn_sched_barrier(0);
     }
-  }
-  float res;
-  if constexpr (MODE == 0) {
-    network_fast<P2, P, P / 2 - 1, P / 2 + 1>(v);
-    res = (n & 1) ? v[P / 2 - 1] : (v[P / 2 - 1] + v[P / 2]) * 0.5f;
-    if (nan_cnt > 0) res = qnan();
-  } else {
-    // lo = int(0.1 n), hi = n - lo over n in (P-16, P]: the kept window is
-    // always inside [int(0.1 (P-15)), P - int(0.1 P)) -> prune the cone to it
-    constexpr int OLO = (P > 16 ? P - 15 : 1) / 10;
-    constexpr int OHI = P - P / 10;
-    network_fast<P2, P, OLO, OHI>(v);
-    float acc = 0.f;
 #pragma unroll
-    for (int p = OLO; p < OHI; ++p) {
-      if (p >= lo && p < hi) {
-        asm volatile("");
-        acc += v[p];
+    for (int i = kFirstPad; i < P; ++i) {
+      // lane i % 64 of block i / 64 holds rows[min(i, n - 1)] (clamped above)
+      const float x = load(i);
+      __builtin_amdgcn_sched_barrier(0);
+      const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
+      v[i] = i < n ? x : pad;
+    }
+    // NaN detection over all slots (pads are +-inf, never NaN)
+    float m = v[0];
+#pragma unroll
+    for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, v[i]);
+    int nan_cnt = 0;
+    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const bool isn = __builtin_isnan(v[i]);
+        nan_cnt += isn ? 1 : 0;
+        v[i] = isn ? __builtin_inff() : v[i];
       }
     }
-    res = acc / static_cast<float>(hi - lo);
-    if (nan_cnt > n - hi) res = qnan();
+    float res;
+    if constexpr (MODE == 0) {
+      network_fast<P2, P, P / 2 - 1, P / 2 + 1>(v);
+      res = (n & 1) ? v[P / 2 - 1] : (v[P / 2 - 1] + v[P / 2]) * 0.5f;
+      if (nan_cnt > 0) res = qnan();
+    } else {
+      // lo = int(0.1 n), hi = n - lo over n in (P-16, P]: the kept window is
+      // always inside [int(0.1 (P-15)), P - int(0.1 P)) -> prune the cone to it
+      constexpr int OLO = (P > 16 ? P - 15 : 1) / 10;
+      constexpr int OHI = P - P / 10;
+      network_fast<P2, P, OLO, OHI>(v);
+      // lo / hi re-materialised per tile: hoisted out of the tile loop, the
+      // ~100 per-slot conditions would be kept as SGPR masks (and spilled)
+      int lo_t = lo, hi_t = hi;
+      asm volatile("" : "+s"(lo_t), "+s"(hi_t));
+      float acc_s = 0.f;
+#pragma unroll
+      for (int p = OLO; p < OHI; ++p) {
+        if (p >= lo_t && p < hi_t) {
+          asm volatile("");
+          acc_s += v[p];
+        }
+      }
+      res = acc_s / static_cast<float>(hi - lo);
+      if (nan_cnt > n - hi) res = qnan();
+    }
+    if (t < rem) out[base + t] = res;
+    // step 2: squared distances of the listed rows over this wave's 64 coordinates
+    const bool valid = t < rem;   // lanes past d contribute 0
+    // fresh copies of the row list: the first pass's 128 readlane results
+    // (SGPRs) must not stay live across the network
+#pragma unroll
+    for (int q = 0; q < RW; ++q) asm volatile("" : "+v"(rl[q]));
+    const unsigned ti = lane & 31u, th = lane >> 5;
+#pragma unroll
+    for (int c = 0; c < RW * 2; ++c) {
+      if (32 * c >= n) break;   // wave-uniform
+      // all loads of the chunk in flight before the first use, unconditional
+      // (rows past n are clamped copies of row n - 1; their sums are never
+      // read): a per-row branch would serialise them on the cache latency
+      constexpr int kChunkRows = 32;
+      float xs[kChunkRows];
+#pragma unroll
+      for (int i = 0; i < kChunkRows; ++i) {
+        if (32 * c + i < P) {
+          xs[i] = load(32 * c + i, true);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kChunkRows; ++i) {
+        if (32 * c + i < P) dl[w][i][lane] = res - xs[i];
+      }
+      if (rem < 256 && !valid) {   // ragged last tile only: lanes past d add 0
+#pragma unroll
+        for (int i = 0; i < 32; ++i) dl[w][i][lane] = 0.f;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float sh = 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(&dl[w][ti][32 * th + 4 * u]);
+        sh = __builtin_fmaf(q[0], q[0], sh);
+        sh = __builtin_fmaf(q[1], q[1], sh);
+        sh = __builtin_fmaf(q[2], q[2], sh);
+        sh = __builtin_fmaf(q[3], q[3], sh);
+      }
+      const float so = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(static_cast<int>((lane ^ 32u) * 4u),
+                                                                              __builtin_bit_cast(int, sh)));
+      const float st = th == 0 ? sh + so : so + sh;   // same value in both halves
+      if (th == 0 && 32 * c + static_cast<int>(ti) < n) wsum[w][32 * c + ti] = st;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();   // dl is rewritten by the next chunk only after every lane read it
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    if (static_cast<int>(t) < n) bs += (wsum[0][t] + wsum[1][t]) + (wsum[2][t] + wsum[3][t]);
+    __syncthreads();   // wsum / dl reuse by the next tile
   }
-  if (t < rem) out[base + t] = res;
+  if (static_cast<int>(t) < n_out) bpart[static_cast<int64_t>(t) * nb + blockIdx.x] = bs;
 }
 
-// ---------------------------------------------------------------------------
-// squared L2 distance of every listed row to `agg`: partial sums per
-// (row position, coordinate chunk), fp32 within a chunk, reduced in fp64 in a
-// fixed order by bulyan_pick_kernel.
-// ---------------------------------------------------------------------------
-constexpr int kDistChunks = 128;
-
-template <bool VEC>  // VEC: rows and agg 16-byte aligned and chunk % 4 == 0
-__global__ void __launch_bounds__(256) row_dist_partial_kernel(const float* __restrict__ X, int64_t ldx,
-                                                               const int* __restrict__ rows, int64_t d,
-                                                               const float* __restrict__ agg, int64_t chunk,
-                                                               float* __restrict__ partial) {
-  const int c = blockIdx.x;      // coordinate chunk
-  const int rp = blockIdx.y;     // position in the row list
-  const float* x = X + static_cast<int64_t>(rows[rp]) * ldx;
-  const int64_t j0 = static_cast<int64_t>(c) * chunk;
-  const int64_t j1 = j0 + chunk < d ? j0 + chunk : d;
-  float s = 0.f;
-  if constexpr (VEC) {
-    // 4 independent float4 loads per thread in flight (16 KB per block step)
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int64_t j = j0 + 4 * threadIdx.x;
-    for (; j + 3 * 1024 + 3 < j1; j += 4 * 1024) {
-      f32x4 xa[4], aa[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        xa[u] = *reinterpret_cast<const f32x4*>(x + j + 1024 * u);
-        aa[u] = *reinterpret_cast<const f32x4*>(agg + j + 1024 * u);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const f32x4 df = aa[u] - xa[u];
-        s0 = __builtin_fmaf(df[0], df[0], s0);
-        s1 = __builtin_fmaf(df[1], df[1], s1);
-        s2 = __builtin_fmaf(df[2], df[2], s2);
-        s3 = __builtin_fmaf(df[3], df[3], s3);
-      }
-    }
-    for (; j + 3 < j1; j += 1024) {
-      const f32x4 df = *reinterpret_cast<const f32x4*>(agg + j) - *reinterpret_cast<const f32x4*>(x + j);
-      s0 = __builtin_fmaf(df[0], df[0], s0);
-      s1 = __builtin_fmaf(df[1], df[1], s1);
-      s2 = __builtin_fmaf(df[2], df[2], s2);
-      s3 = __builtin_fmaf(df[3], df[3], s3);
-    }
-    for (int64_t q = j; q < j1 && q < j + 4; ++q) {   // ragged tail of the chunk
-      const float df = agg[q] - x[q];
-      s0 = __builtin_fmaf(df, df, s0);
-    }
-    s = (s0 + s1) + (s2 + s3);
-  } else {
-    for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
-      const float df = agg[j] - x[j];
-      s = __builtin_fmaf(df, df, s);
-    }
-  }
-  // block reduce (fixed order)
-  __shared__ float red[256];
+// dist[r] = the per-block partials of listed row r summed in block order
+// (fp64): a strided sequential sum per thread, then a fixed tree
+__global__ void __launch_bounds__(256) bulyan_dist_reduce_kernel(const float* __restrict__ bpart, int nb,
+                                                                 double* __restrict__ dist) {
+  const int r = blockIdx.x;
+  const float* p = bpart + static_cast<int64_t>(r) * nb;
+  double s = 0.0;
+  for (int g = threadIdx.x; g < nb; g += 256) s += static_cast<double>(p[g]);
+  __shared__ double red[256];
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < static_cast<unsigned>(k)) red[threadIdx.x] += red[threadIdx.x + k];
     __syncthreads();
   }
-  if (threadIdx.x == 0) partial[static_cast<int64_t>(rp) * kDistChunks + c] = red[0];
+  if (threadIdx.x == 0) dist[r] = red[0];
 }
 
-// RB rows of the list per block over one coordinate chunk: the aggregate's
-// float4 is loaded once for RB rows (it used to be re-read by every row's
-// block), the rows are streamed with non-temporal loads.  Per row the
-// accumulation order is exactly row_dist_partial_kernel<true>'s (elements j,
-// j+1024, ... into four component sums, then the same fixed tree), so the
-// partial sums are bit-identical.
-template <int RB>
-__global__ void __launch_bounds__(256) row_dist_multi_kernel(const float* __restrict__ X, int64_t ldx,
-                                                            const int* __restrict__ rows, int nr, int64_t d,
-                                                            const float* __restrict__ agg, int64_t chunk,
-                                                            float* __restrict__ partial) {
-  const int c = blockIdx.x;
-  const int rp0 = blockIdx.y * RB;
-  const f32x4* x[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    const int rr = rp0 + r < nr ? rp0 + r : nr - 1;
-    x[r] = reinterpret_cast<const f32x4*>(X + static_cast<int64_t>(rows[rr]) * ldx);
-  }
-  const f32x4* a4 = reinterpret_cast<const f32x4*>(agg);
-  const int64_t j0 = static_cast<int64_t>(c) * chunk;
-  const int64_t j1 = j0 + chunk < d ? j0 + chunk : d;
-  float s[RB][4];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) s[r][0] = s[r][1] = s[r][2] = s[r][3] = 0.f;
-  int64_t j = j0 + 4 * threadIdx.x;
-  for (; j + 1024 + 3 < j1; j += 2 * 1024) {
-    f32x4 aa[2], xa[RB][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      aa[u] = a4[(j + 1024 * u) / 4];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) xa[r][u] = __builtin_nontemporal_load(x[r] + (j + 1024 * u) / 4);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const f32x4 df = aa[u] - xa[r][u];
-        s[r][0] = __builtin_fmaf(df[0], df[0], s[r][0]);
-        s[r][1] = __builtin_fmaf(df[1], df[1], s[r][1]);
-        s[r][2] = __builtin_fmaf(df[2], df[2], s[r][2]);
-        s[r][3] = __builtin_fmaf(df[3], df[3], s[r][3]);
-      }
-    }
-  }
-  for (; j + 3 < j1; j += 1024) {
-    const f32x4 aa = a4[j / 4];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const f32x4 df = aa - __builtin_nontemporal_load(x[r] + j / 4);
-      s[r][0] = __builtin_fmaf(df[0], df[0], s[r][0]);
-      s[r][1] = __builtin_fmaf(df[1], df[1], s[r][1]);
-      s[r][2] = __builtin_fmaf(df[2], df[2], s[r][2]);
-      s[r][3] = __builtin_fmaf(df[3], df[3], s[r][3]);
-    }
-  }
-  for (int64_t q = j; q < j1 && q < j + 4; ++q) {   // ragged tail of the chunk
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const float df = agg[q] - reinterpret_cast<const float*>(x[r])[q];
-      s[r][0] = __builtin_fmaf(df, df, s[r][0]);
-    }
-  }
-  __shared__ float red[RB][256];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) red[r][threadIdx.x] = (s[r][0] + s[r][1]) + (s[r][2] + s[r][3]);
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) {
-#pragma unroll
-      for (int r = 0; r < RB; ++r) red[r][threadIdx.x] += red[r][threadIdx.x + w];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x < RB && rp0 + static_cast<int>(threadIdx.x) < nr)
-    partial[static_cast<int64_t>(rp0 + threadIdx.x) * kDistChunks + c] = red[threadIdx.x][0];
+static int64_t round_tiles_per_block(int64_t d) { return cdiv(cdiv(d, 256), kRoundMaxBlocks); }
+static int64_t round_blocks(int64_t d) { return cdiv(cdiv(d, 256), round_tiles_per_block(d)); }
+static size_t round_partial_bytes(int n, int64_t d) {
+  return sizeof(float) * static_cast<size_t>(n) * static_cast<size_t>(round_blocks(d));
 }
-
-// fp64 distance of every listed row: its chunk partials summed in chunk order
-__global__ void __launch_bounds__(256) bulyan_dist_kernel(const float* __restrict__ partial, int nr, int nchunks,
-                                                          double* __restrict__ dist) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nr) return;
-  double s = 0.0;
-  for (int c = 0; c < nchunks; ++c) s += static_cast<double>(partial[static_cast<int64_t>(r) * kDistChunks + c]);
-  dist[r] = s;
-}
+constexpr size_t kRoundPartialMaxBytes = sizeof(float) * 128 * kRoundMaxBlocks;
 
 // argmin (first strict minimum, NaN never chosen) of the listed rows'
 // distances; removes it from the list (order preserved) into rows_next.
@@ -747,7 +726,7 @@ static size_t bulyan_body_bytes(int n, int64_t d, int mode, int f) {
     b += krum_workspace_bytes(n, d);
   } else {
     b += sizeof(float) * static_cast<size_t>(theta > 0 ? theta : 0) * static_cast<size_t>(d) + 256;
-    b += sizeof(float) * static_cast<size_t>(n) * kDistChunks + sizeof(double) * static_cast<size_t>(n) + 256;
+    b += round_partial_bytes(n, d) + sizeof(double) * static_cast<size_t>(n) + 512;
   }
   return (b + 255) / 256 * 256;
 }
@@ -757,15 +736,16 @@ size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
 }
 
 template <int MODE>
-static int launch_select_rows(const float* X, int64_t ldx, const int* rows, int n, int64_t d, int lo, int hi,
-                              float* out, hipStream_t s) {
-  const int64_t blocks = cdiv(d, 256);
+static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int n, int64_t d, int lo, int hi,
+                              float* out, float* bpart, hipStream_t s) {
+  const int64_t tpb = round_tiles_per_block(d);
+  const int64_t blocks = round_blocks(d);
   const int P = static_cast<int>(cdiv(n, 16) * 16);
-#define SRA_SR(PP)                                                                                               \
-  case PP:                                                                                                       \
-    hipLaunchKernelGGL((select_rows_kernel<PP, MODE>), dim3(blocks), dim3(256), 0, s, X, ldx, rows, n, d, lo, hi, \
-                       out);                                                                                     \
-    return launch_status("select_rows_kernel");
+#define SRA_SR(PP)                                                                                             \
+  case PP:                                                                                                     \
+    hipLaunchKernelGGL((select_dist_rows_kernel<PP, MODE>), dim3(blocks), dim3(256), 0, s, X, ldx, rows, n, d, lo, \
+                       hi, out, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                       \
+    return launch_status("select_dist_rows_kernel");
   switch (P) {
     SRA_SR(16) SRA_SR(32) SRA_SR(48) SRA_SR(64) SRA_SR(80) SRA_SR(96) SRA_SR(112) SRA_SR(128)
     default: break;
@@ -804,37 +784,36 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int theta
 // One selection round of Bulyan's median / trimmed-mean modes
 // (robust_estimator.py:297-322) over the listed rows: agg = the coordinate-wise
 // aggregate of the remaining clients, dist[r] = squared L2 distance of listed
-// row r to it (fp32 within each of kDistChunks coordinate chunks, fp64 across
-// them in chunk order).  Over a column shard, dist is this shard's share: the
-// shards' dist vectors sum (all-reduce) to the distance over all columns.
+// row r to it (fp32 within a 256-coordinate block, fp64 across blocks in
+// order), both from ONE pass over the rows.  Over a column shard, dist is this
+// shard's share: the shards' dist vectors sum (all-reduce) to the distance
+// over all columns.  bpart: nr x round_blocks(d) floats.
 static int launch_bulyan_round(const float* X, int64_t d, int64_t ldx, const int* rows, int nr, int mode, bool dba,
-                               float* agg, float* partial, double* dist, hipStream_t s) {
-  int rc;
+                               float* agg, float* bpart, double* dist, hipStream_t s) {
+  int lo, hi, sel_mode;
   if (mode == kBulyanMedian && dba) {
-    const int k = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
-    rc = launch_select_rows<1>(X, ldx, rows, nr, d, k, k + 1, agg, s);
+    lo = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
+    hi = lo + 1;
+    sel_mode = 1;
   } else if (mode == kBulyanMedian) {
-    rc = launch_select_rows<0>(X, ldx, rows, nr, d, 0, nr, agg, s);
+    lo = 0;
+    hi = nr;
+    sel_mode = 0;
   } else {
     const int b = static_cast<int>(nr * 0.1);  // trimmed_mean(beta=0.1): int(size * beta)
-    const int lo = b, hi = nr - b > b ? nr - b : b;
-    rc = launch_select_rows<1>(X, ldx, rows, nr, d, lo, hi, agg, s);
+    lo = b;
+    hi = nr - b > b ? nr - b : b;
+    sel_mode = 1;
   }
-  if (rc) return rc;
-  const int64_t chunk = cdiv(cdiv(d, kDistChunks), 4) * 4;
-  const int nchunks = static_cast<int>(cdiv(d, chunk));
-  const bool dist_vec = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && (ldx % 4 == 0) && (d % 4 == 0) &&
-                        (reinterpret_cast<uintptr_t>(agg) % 16 == 0);
-  if (dist_vec)
-    hipLaunchKernelGGL(row_dist_multi_kernel<4>, dim3(nchunks, cdiv(nr, 4)), dim3(256), 0, s, X, ldx, rows, nr, d,
-                       agg, chunk, partial);
+  int rc;
+  if (sel_mode == 0)
+    rc = launch_select_dist<0>(X, ldx, rows, nr, d, lo, hi, agg, bpart, s);
   else
-    hipLaunchKernelGGL(row_dist_partial_kernel<false>, dim3(nchunks, nr), dim3(256), 0, s, X, ldx, rows, d, agg,
-                       chunk, partial);
-  rc = launch_status("row_dist_partial_kernel");
+    rc = launch_select_dist<1>(X, ldx, rows, nr, d, lo, hi, agg, bpart, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(bulyan_dist_kernel, dim3(cdiv(nr, 256)), dim3(256), 0, s, partial, nr, nchunks, dist);
-  return launch_status("bulyan_dist_kernel");
+  hipLaunchKernelGGL(bulyan_dist_reduce_kernel, dim3(nr), dim3(256), 0, s, bpart, static_cast<int>(round_blocks(d)),
+                     dist);
+  return launch_status("bulyan_dist_reduce_kernel");
 }
 
 __global__ void iota_kernel(int* p, int n) {
@@ -871,19 +850,21 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   }
   SRA_REQUIRE(n <= 128, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= 128 (got %d)", n);
   float* S = reinterpret_cast<float*>(rest);
-  float* partial = S + static_cast<size_t>(theta) * static_cast<size_t>(d) + 64;
+  float* bpart = reinterpret_cast<float*>(
+      (reinterpret_cast<uintptr_t>(S + static_cast<size_t>(theta) * static_cast<size_t>(d)) + 255) &
+      ~static_cast<uintptr_t>(255));
   hipLaunchKernelGGL(iota_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, rows_a, n);
   hipLaunchKernelGGL(iota_kernel, dim3(cdiv(theta, 256)), dim3(256), 0, s, order, theta);
   rc = launch_status("iota_kernel");
   if (rc) return rc;
   double* dist = reinterpret_cast<double*>(
-      (reinterpret_cast<uintptr_t>(partial + static_cast<size_t>(n) * kDistChunks) + 255) & ~static_cast<uintptr_t>(255));
+      (reinterpret_cast<uintptr_t>(bpart) + round_partial_bytes(n, d) + 255) & ~static_cast<uintptr_t>(255));
   int* cur = rows_a;
   int* nxt = rows_b;
   for (int t = 0; t < theta; ++t) {
     const int nr = n - t;
     float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
-    rc = launch_bulyan_round(X, d, ldx, cur, nr, mode, dba, agg, partial, dist, s);
+    rc = launch_bulyan_round(X, d, ldx, cur, nr, mode, dba, agg, bpart, dist, s);
     if (rc) return rc;
     hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, dist, cur, nr, nxt, status);
     rc = launch_status("bulyan_pick_kernel");
@@ -973,7 +954,7 @@ extern "C" int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, in
 extern "C" int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
   SRA_REQUIRE(n >= 1 && n <= 128, SRA_ERR_UNSUPPORTED, "bulyan rounds support 1 <= N <= 128");
-  *bytes = sizeof(float) * static_cast<size_t>(n) * kDistChunks + 256;
+  *bytes = kRoundPartialMaxBytes + 256;
   return SRA_OK;
 }
 

@@ -442,7 +442,9 @@ __device__ __forceinline__ float sort4_blocks_nancheck(float (&v)[P2]) {
     const float s0 = __builtin_fminf(__builtin_fminf(a0, a1), a2);
     const float s1 = __builtin_amdgcn_fmed3f(a0, a1, a2);
     const float s2 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a0, a1), a2);
-    v[b] = __builtin_fminf(s0, d);
+    // IEEE-754-2019 minimum: no operand canonicalisation (fminf of a loaded
+    // value costs an extra v_max_f32 x, x, x per block in IEEE mode)
+    v[b] = __builtin_elementwise_minimum(s0, d);
     v[b + 1] = __builtin_amdgcn_fmed3f(s0, s1, d);
     v[b + 2] = __builtin_amdgcn_fmed3f(s1, s2, d);
     v[b + 3] = __builtin_elementwise_maximum(s2, d);

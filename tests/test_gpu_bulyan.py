@@ -56,7 +56,7 @@ def test_golden_bulyan(rec):
 
 
 @pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
-@pytest.mark.parametrize("n,f", [(100, 20), (64, 10), (37, 8), (100, 30), (30, 8)])
+@pytest.mark.parametrize("n,f", [(128, 20), (100, 20), (64, 10), (37, 8), (100, 30), (30, 8), (16, 3)])
 def test_bulyan_against_oracle(mode, n, f):
     x = make_rows(n, 1500, seed=77 + n + f, byz=f)
     want, _ = _leftfirst_and_ties(list(x), f, mode)
