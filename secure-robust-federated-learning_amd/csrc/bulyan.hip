@@ -78,7 +78,7 @@ __device__ __forceinline__ float ld_lane(const char* row, unsigned off) {
 constexpr int kRoundMaxBlocks = 65536;
 
 template <int P, int MODE>  // MODE: 0 median, 1 trimmed; n in (P-16, P] (P=16: 1..16)
-__global__ void __launch_bounds__(256) select_dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
+__global__ void __launch_bounds__(256, 3) select_dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
                                                                const int* __restrict__ rows, int n_arg, int64_t d,
                                                                int lo, int hi, float* __restrict__ out,
                                                                float* __restrict__ bpart, int nb, int tpb) {
@@ -126,7 +126,8 @@ __global__ void __launch_bounds__(256) select_dist_rows_kernel(const float* __re
       // default cache policy (not nt): step 2 re-reads these lines.  A/B at
       // N=128, d=1e7: 2.06 ms (default) vs 2.14 (nt) per P=128 round; keeping
       // an unsorted copy in registers instead (AGPR-backed): 2.63 ms
-      return *reinterpret_cast<const float*>(rp + off);
+      typedef const __attribute__((address_space(1))) float gfloat;
+      return *reinterpret_cast<gfloat*>(reinterpret_cast<uint64_t>(rp) + off);   // global_load, SGPR base
     };
     constexpr int kFirstPad = P > 16 ? P - 16 : 0;   // rows below this are always real (n > P - 16)
     float v[P2];
@@ -240,14 +241,22 @@ __global__ void __launch_bounds__(256) select_dist_rows_kernel(const float* __re
   if (static_cast<int>(t) < n_out) bpart[static_cast<int64_t>(t) * nb + blockIdx.x] = bs;
 }
 
-// dist[r] = the per-block partials of listed row r summed in block order
-// (fp64): a strided sequential sum per thread, then a fixed tree
+// dist[r] = the per-block partials of listed row r summed in fp64 in a fixed
+// order: strided chains per thread, then a fixed tree
 __global__ void __launch_bounds__(256) bulyan_dist_reduce_kernel(const float* __restrict__ bpart, int nb,
                                                                  double* __restrict__ dist) {
   const int r = blockIdx.x;
   const float* p = bpart + static_cast<int64_t>(r) * nb;
-  double s = 0.0;
-  for (int g = threadIdx.x; g < nb; g += 256) s += static_cast<double>(p[g]);
+  // eight independent strided chains per thread (loads in flight), combined
+  // in a fixed order
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int g = threadIdx.x;
+  for (; g + 7 * 256 < nb; g += 8 * 256) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += static_cast<double>(p[g + 256 * u]);
+  }
+  for (; g < nb; g += 256) a[0] += static_cast<double>(p[g]);
+  double s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __shared__ double red[256];
   red[threadIdx.x] = s;
   __syncthreads();

@@ -1,0 +1,21 @@
+#!/bin/bash
+# bucket-mean kernel + north-star recheck
+set -u
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/r2b
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$R"
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_krum.py tests/test_gpu_filters.py tests/test_gpu_dispatch.py > "$OUT/pytest.log" 2>&1 || { echo "pytest failed"; tail -30 "$OUT/pytest.log"; exit 1; }
+tail -1 "$OUT/pytest.log"
+for a in "mom_krum --clients 512 --d 1.25e7" "trimmedmean --steps 20" "trimmedmean --steps 20" "bulyantrimmedmean --d 1e7 --steps 3" "bulyanmedian --d 1e7 --steps 3"; do
+  timeout -k 10 240 python bench.py --warmup 2 --no-host --no-cpu --agg $a > "$OUT/b.log" 2>&1 || { echo "bench $a failed"; tail -5 "$OUT/b.log"; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('$OUT/b.log').read().strip().splitlines()[-1]); r=d['roofline']
+print('$a', d['ms_per_step'], r['kernel_ms'], r['frac'])"
+done
+cd /tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_momkrum" -o run -- python3 "$R/bench.py" --warmup 1 --no-cpu --no-host --agg mom_krum --clients 512 --d 1.25e7 --steps 5 > "$OUT/prof.log" 2>&1 || { echo "prof failed"; exit 1; }
+python3 -c "
+import csv
+for x in list(csv.DictReader(open('$OUT/prof_momkrum/run_kernel_stats.csv')))[:5]: print(x['Name'][:60], x['Calls'], float(x['AverageNs'])/1e6)"
