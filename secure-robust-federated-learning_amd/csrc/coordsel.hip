@@ -18,7 +18,7 @@
 //
 // Roofline: HBM-bound, 4*N*d + 4*d bytes per call.  The exact-N trimmed mean
 // at N=128 (select_plain_kernel) runs a network pruned to the kept ranks
-// (network_fast); its VALU instruction count per tile is reported by
+// (4-blocks + network_plain); its VALU instruction count per tile is reported by
 // tools/isa_stats.py and set against the HBM time in DESIGN.md §3.
 //
 // 128 < N <= 512 (the N=512 MoM / 8-GPU config) uses 2 or 4 lanes per
