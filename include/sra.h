@@ -265,6 +265,14 @@ int sra_attack_krum_workspace_bytes(int64_t m, int64_t d, double lower_bound, si
 int sra_attack_krum_f32(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
                         const int32_t* benign_rows, int32_t nbenign, double lower_bound, double* mal_row,
                         double* lam_out, int32_t* chosen_out, void* ws, size_t ws_bytes, void* stream);
+/* bulyan_attack_krum (src/attack.py:264-308): the same lambda search with the
+ * caller's direction dir (d floats; the reference's attack_vec[param_index]:
+ * ones for the target layer, zeros elsewhere) in place of the benign sign.
+ * Malicious rows = -lambda * dir (float64).  Workspace as sra_attack_krum_f32. */
+int sra_attack_krum_dir_f32(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
+                            const int32_t* benign_rows, int32_t nbenign, const float* dir, double lower_bound,
+                            double* mal_row, double* lam_out, int32_t* chosen_out, void* ws, size_t ws_bytes,
+                            void* stream);
 
 /* Python's `random` stream (MT19937, genrand_uint32) on the device: state_in =
  * random.getstate()[1] as 625 uint32 (624 words + position); writes the nwords

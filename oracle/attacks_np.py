@@ -67,6 +67,32 @@ def attack_krum(local_grads, mal_index, param_index, lower_bound=1e-8):
     return lam, -lam * s
 
 
+def bulyan_attack_krum(shapes, local_grads, mal_index, param_index, lower_bound=1e-8, target_layer=0,
+                       target_idx=0):
+    """attack.py:264-308: attack_vec[idx] (np.zeros of the network's layer
+    shapes) gets + 1 once for idx == target_idx when some c in
+    range(#benign) equals target_layer (:278-282); lambda runs 1, 1/2, ...
+    (upper_bound overwritten at :286) until krum(f=1) picks a malicious row or
+    lambda < lower_bound; the malicious rows become -lambda * attack_vec.
+    ``shapes`` = the network's parameter shapes.  Returns (lambda, row)."""
+    m = len(local_grads)
+    nben = len(_benign(m, mal_index))
+    vec = np.zeros(shapes[param_index])
+    if param_index == target_idx and 0 <= target_layer < nben:
+        vec = vec + 1
+    mal = set(int(i) for i in mal_index)
+    lam = 1.0
+    while True:
+        cand = [(-lam * vec) if c in mal else local_grads[c][param_index] for c in range(m)]
+        pick = krum_pick_mixed(cand, 1)
+        if pick in mal or lam < lower_bound:
+            break
+        lam /= 2.0
+    for kk in mal_index:
+        local_grads[kk][param_index] = -lam * vec
+    return lam, -lam * vec
+
+
 def attack_trimmedmean(params, local_grads, mal_index, b=2, rng=random):
     """attack.py:157-198 with NumPy >= 2 scalar promotion: the per-element draw
     is a + (b - a) * r in float32 (a, b float32; the Python floats b and r are

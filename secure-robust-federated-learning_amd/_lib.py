@@ -94,6 +94,8 @@ _SIGS = {
     "sra_clipped_mean_f64": [_ptr, _i64, _i64, _i64, _ptr, _ptr, _ptr, _i64, _ptr, _ptr],
     "sra_attack_krum_workspace_bytes": [_i64, _i64, _dbl, ctypes.POINTER(_sz)],
     "sra_attack_krum_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr, _i32, _dbl, _ptr, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_attack_krum_dir_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr, _i32, _ptr, _dbl, _ptr, _ptr, _ptr, _ptr, _sz,
+                                _ptr],
     "sra_mt19937_words": [_ptr, _i64, _ptr, _ptr, _ptr],
     "sra_attack_trimmedmean_f32": [_ptr, _i64, _i64, _ptr, _i32, _ptr, _ptr, _dbl, _ptr, _ptr],
     "sra_attack_xie_f32": [_ptr, _i64, _i64, _ptr, _i32, _dbl, _i64, _ptr, _ptr],

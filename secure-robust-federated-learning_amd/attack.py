@@ -7,6 +7,9 @@ and in-place semantics:
 * ``attack_trimmedmean(network, local_grads, mal_index, b=2)``  (attack.py:157-198,
   simulate.py:220 with b=1.5)
 * ``attack_xie(local_grads, weight, choices, mal_index)``  (attack.py:362-372)
+* ``bulyan_attack_krum(network, local_grads, mal_index, param_index, lower_bound=1e-8,
+  upper_bound=1e-3, target_layer=0, target_idx=0)``  (attack.py:264-308; defined
+  by the reference but not called by simulate.py)
 
 Each mutates ``local_grads`` in place and returns it, like the reference.  The
 d-dependent work runs in libsra.so (csrc/attack.hip); ``local_grads`` entries
@@ -101,6 +104,50 @@ def attack_krum(network, local_grads, mal_index, param_index, lower_bound=1e-8, 
     X = _stack(layer, torch.float32, dev)
     mask = _i32((1 if c in mal else 0 for c in range(m)), dev)
     row, _, _ = attack_krum_layer(X, mask, _i32(benign, dev), lower_bound)
+    for kk in mal_index:
+        local_grads[kk][param_index] = _emit(row, shape, dev_io)
+    return local_grads
+
+
+def bulyan_attack_krum(network, local_grads, mal_index, param_index, lower_bound=1e-8, upper_bound=1e-3,
+                       target_layer=0, target_idx=0):
+    """attack.py:264-308: attack_krum's lambda search with the direction
+    attack_vec[param_index] in place of the benign sign: ones when
+    ``param_index == target_idx`` and ``target_layer`` indexes a benign client
+    (the reference adds 1 once, for the loop's c == target_layer), zeros
+    otherwise.  The malicious rows become -lambda * attack_vec[param_index]
+    (float64).  ``network`` gives the layer's shape; ``upper_bound`` is
+    overwritten with 1.0 by the reference (:286)."""
+    m = len(local_grads)
+    mal = {int(i) for i in mal_index}
+    benign = [c for c in range(m) if c not in mal]
+    params = [p.data if hasattr(p, "data") else p for p in network.parameters()]
+    shape = tuple(params[param_index].shape)
+    ones = param_index == target_idx and 0 <= int(target_layer) < len(benign)
+    layer = [local_grads[c][param_index] for c in range(m)]
+    dev_io = _on_device(layer[0])
+    if not mal:
+        return local_grads            # the loop runs, but there is no row to write
+    if not benign:
+        # attack_vec is all zeros: every row is -lambda * 0, krum picks row 0 at lambda = 1
+        for kk in mal_index:
+            z = -1.0 * np.zeros(shape)
+            local_grads[kk][param_index] = torch.from_numpy(z).to(layer[0].device) if dev_io else z
+        return local_grads
+    dev = layer[0].device if dev_io else _device()
+    X = _stack(layer, torch.float32, dev)
+    Xm, mm, d, ldx = engine.as_matrix(X)
+    direction = (torch.ones if ones else torch.zeros)(d, dtype=torch.float32, device=dev)
+    mask = _i32((1 if c in mal else 0 for c in range(m)), dev)
+    rows = _i32(benign, dev)
+    nb = _lib.query_bytes("sra_attack_krum_workspace_bytes", mm, d, float(lower_bound))
+    ws = engine._workspace(nb, dev)
+    row = torch.empty(d, dtype=torch.float64, device=dev)
+    lam = torch.empty(1, dtype=torch.float64, device=dev)
+    pick = torch.empty(1, dtype=torch.int32, device=dev)
+    _lib.call("sra_attack_krum_dir_f32", Xm.data_ptr(), mm, d, ldx, mask.data_ptr(), rows.data_ptr(),
+              int(rows.numel()), direction.data_ptr(), float(lower_bound), row.data_ptr(), lam.data_ptr(),
+              pick.data_ptr(), ws.data_ptr(), nb, engine._stream_ptr(dev))
     for kk in mal_index:
         local_grads[kk][param_index] = _emit(row, shape, dev_io)
     return local_grads

@@ -422,9 +422,13 @@ extern "C" int sra_attack_krum_workspace_bytes(int64_t m, int64_t d, double lowe
   return SRA_OK;
 }
 
-extern "C" int sra_attack_krum_f32(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
-                                   const int32_t* benign_rows, int32_t nbenign, double lower_bound, double* mal_row,
-                                   double* lam_out, int32_t* chosen_out, void* ws, size_t ws_bytes, void* stream) {
+// dir == nullptr: attack_krum's direction, the sign of the benign sum
+// (attack.py:211-216); else the caller's (bulyan_attack_krum's attack_vec,
+// attack.py:278-282).  The malicious rows are -lambda * dir.
+static int attack_krum_impl(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
+                            const int32_t* benign_rows, int32_t nbenign, const float* dir, double lower_bound,
+                            double* mal_row, double* lam_out, int32_t* chosen_out, void* ws, size_t ws_bytes,
+                            void* stream) {
   SRA_REQUIRE(X != nullptr && mal_mask != nullptr && benign_rows != nullptr && mal_row != nullptr &&
                   lam_out != nullptr && chosen_out != nullptr && ws != nullptr,
               SRA_ERR_ARG, "null pointer");
@@ -455,9 +459,14 @@ extern "C" int sra_attack_krum_f32(const float* X, int64_t m, int64_t d, int64_t
   p += al256(static_cast<size_t>(mi + 1) * 16);
   int* chosen = reinterpret_cast<int*>(p);
 
-  hipLaunchKernelGGL(sign_sum_kernel, dim3(cdiv(d, kAtkBS)), dim3(kAtkBS), 0, s, X, d, ldx, benign_rows, nb, sg);
-  int rc = launch_status("sign_sum_kernel");
-  if (rc) return rc;
+  int rc;
+  if (dir == nullptr) {
+    hipLaunchKernelGGL(sign_sum_kernel, dim3(cdiv(d, kAtkBS)), dim3(kAtkBS), 0, s, X, d, ldx, benign_rows, nb, sg);
+    rc = launch_status("sign_sum_kernel");
+    if (rc) return rc;
+  } else {
+    SRA_HIP(hipMemcpyAsync(sg, dir, sizeof(float) * static_cast<size_t>(d), hipMemcpyDeviceToDevice, s));
+  }
   rc = launch_gram(X, mi, d, ldx, G, slab, slab_bytes, s);
   if (rc) return rc;
   hipLaunchKernelGGL(sa_partial_kernel, dim3(ntiles, nb + 1), dim3(kAtkBS), 0, s, X, d, ldx, benign_rows, nb, sg,
@@ -481,6 +490,22 @@ extern "C" int sra_attack_krum_f32(const float* X, int64_t m, int64_t d, int64_t
   if (rc) return rc;
   hipLaunchKernelGGL(attack_krum_row_kernel, dim3(cdiv(d, kAtkBS)), dim3(kAtkBS), 0, s, sg, d, lam_out, mal_row);
   return launch_status("attack_krum_row_kernel");
+}
+
+extern "C" int sra_attack_krum_f32(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
+                                   const int32_t* benign_rows, int32_t nbenign, double lower_bound, double* mal_row,
+                                   double* lam_out, int32_t* chosen_out, void* ws, size_t ws_bytes, void* stream) {
+  return attack_krum_impl(X, m, d, ldx, mal_mask, benign_rows, nbenign, nullptr, lower_bound, mal_row, lam_out,
+                          chosen_out, ws, ws_bytes, stream);
+}
+
+extern "C" int sra_attack_krum_dir_f32(const float* X, int64_t m, int64_t d, int64_t ldx, const int32_t* mal_mask,
+                                       const int32_t* benign_rows, int32_t nbenign, const float* dir,
+                                       double lower_bound, double* mal_row, double* lam_out, int32_t* chosen_out,
+                                       void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(dir != nullptr, SRA_ERR_ARG, "null direction");
+  return attack_krum_impl(X, m, d, ldx, mal_mask, benign_rows, nbenign, dir, lower_bound, mal_row, lam_out,
+                          chosen_out, ws, ws_bytes, stream);
 }
 
 extern "C" int sra_mt19937_words(const uint32_t* state_in, int64_t nwords, uint32_t* words, uint32_t* state_out,

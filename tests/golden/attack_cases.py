@@ -32,6 +32,11 @@ CASES = [
      "pre_words": 37, "seed": 905},
     {"name": "xie_A", "func": "attack_xie", "m": 30, "mal": list(range(6)), "perround": 20, "weight": 1,
      "seed": 906},
+    # bulyan_attack_krum (attack.py:264-308), target_layer / target_idx defaults and a non-default target
+    {"name": "bkrum_A", "func": "bulyan_attack_krum", "m": 30, "mal": list(range(6)), "lower_bound": 1e-8,
+     "target_layer": 0, "target_idx": 0, "seed": 907},
+    {"name": "bkrum_B", "func": "bulyan_attack_krum", "m": 24, "mal": [2, 5, 11, 23], "lower_bound": 1e-5,
+     "target_layer": 3, "target_idx": 1, "seed": 908},
 ]
 
 

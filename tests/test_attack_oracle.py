@@ -26,6 +26,18 @@ def _cases(func):
     return [c for c in CASES if c["func"] == func]
 
 
+@pytest.mark.parametrize("case", _cases("bulyan_attack_krum"), ids=lambda c: c["name"])
+def test_bulyan_attack_krum_oracle_matches_reference(case):
+    fx = load_fixture(case)
+    grads, params = case_clients(case)
+    shapes = [p.shape for p in params]
+    for idx in range(len(params)):
+        orc.bulyan_attack_krum(shapes, grads, case["mal"], idx, case["lower_bound"], case["target_layer"],
+                               case["target_idx"])
+    for k, c in enumerate(case["mal"]):
+        np.testing.assert_array_equal(_flat(grads[c]), fx["mal_out"][k])
+
+
 @pytest.mark.parametrize("case", _cases("attack_krum"), ids=lambda c: c["name"])
 def test_attack_krum_oracle_matches_reference(case):
     fx = load_fixture(case)

@@ -61,6 +61,30 @@ def test_mt19937_words_equal_python_random(seed, pre, n):
 
 
 @pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
+@pytest.mark.parametrize("case", _cases("bulyan_attack_krum"), ids=lambda c: c["name"])
+def test_bulyan_attack_krum_matches_reference(case, device):
+    """attack.py:264-308 (not called by simulate.py): the live reference's rows,
+    the target layer's ones-direction and the other layers' zero (-0.0) rows."""
+    from srfl_amd import attack
+    fx = load_fixture(case)
+    grads, params = case_clients(case)
+    if device:
+        grads = _to_dev(grads)
+    net = _Net(params)
+    for idx in range(len(params)):
+        ret = attack.bulyan_attack_krum(net, grads, case["mal"], idx, lower_bound=case["lower_bound"],
+                                        target_layer=case["target_layer"], target_idx=case["target_idx"])
+        assert ret is grads
+    for k, c in enumerate(case["mal"]):
+        got = _flat(grads[c])
+        np.testing.assert_array_equal(got, fx["mal_out"][k])
+        np.testing.assert_array_equal(np.signbit(got), np.signbit(fx["mal_out"][k]))
+        assert all((a.dtype == torch.float64) if device else (a.dtype == np.float64) for a in grads[c])
+    benign = [c for c in range(case["m"]) if c not in set(case["mal"])]
+    np.testing.assert_array_equal(np.stack([_flat(grads[c]) for c in benign]), fx["benign_out"])
+
+
+@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
 @pytest.mark.parametrize("case", _cases("attack_krum"), ids=lambda c: c["name"])
 def test_attack_krum_matches_reference(case, device):
     from srfl_amd import attack
