@@ -214,6 +214,14 @@ def solver_flops(agg, X, itv=1000):
     return per_chunk * nchunks, iters
 
 
+def filter_block(d, chunks, itv):
+    """Block width for the pipelined filter path: d split into the largest
+    number <= chunks of equal blocks that are whole itv-chunks (the filters
+    chunk every layer at itv, robust_estimator.py:116-125); 0 if none."""
+    nblk = next((c for c in range(int(chunks), 0, -1) if d % (c * itv) == 0), 0)
+    return d // nblk if nblk else 0
+
+
 def cpu_baseline(agg, n, budget_s):
     """Time the oracle's CPU port on a bounded sample until ~budget_s elapsed."""
     from oracle import robust_np as orc
@@ -331,11 +339,9 @@ def main():
     # coordinates are independent (robust_estimator.py:116-125, 192-201), so
     # the same block-cyclic pipeline runs with itv-aligned blocks
     if world > 1 and a.agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
-        itv = FILTER_ARGS["itv"]
-        nblk = next((c for c in range(a.chunks, 0, -1) if d % (c * itv) == 0), 0)
-        if nblk:
+        block = filter_block(d, a.chunks, FILTER_ARGS["itv"])
+        if block:
             pipelined = True
-            block = d // nblk
             into = lambda Xc, o: o.copy_(fn_into(Xc))   # noqa: E731
             ffn = {"filterl2": engine.filter_l2, "ex_noregret": engine.ex_noregret,
                    "mom_filterl2": engine.mom_filter_l2, "mom_ex_noregret": engine.mom_ex_noregret}[a.agg]

@@ -140,6 +140,22 @@ def _worker(rank, world, port, results):
             def tm_into(X, o):
                 o.copy_(torch.from_numpy(np.asarray(orc.trimmed_mean(list(X.numpy())))))
             out["cyclic_%d" % block] = shard.pipelined_coordinatewise(tm_into, Xc, d, block).numpy().copy()
+        # config C5's bench path: mom_filterL2 on a block-cyclic shard whose
+        # blocks are whole itv-chunks (bench.filter_block), pipelined all-gather
+        import bench
+        itv, dl = 40, 160
+        dt = dl * world
+        xc5 = make_rows(24, dt, seed=14, byz=4)
+        block = bench.filter_block(dl, 4, itv)
+        cols = shard.cyclic_blocks(dt, world, rank, block)
+        Xc5 = torch.from_numpy(np.ascontiguousarray(np.concatenate([xc5[:, lo:hi] for lo, hi in cols], axis=1)))
+
+        def mom_into(X, o):
+            o.copy_(torch.from_numpy(np.asarray(orc.mom_filterL2(list(X.numpy()), 0.2, 0.02, 20, itv,
+                                                                 float(np.exp(-2.0)))).ravel()))
+        mom_into.out_dtype = torch.float64
+        out["c5_block"] = block
+        out["c5"] = shard.pipelined_coordinatewise(mom_into, Xc5, dt, block).numpy().copy()
         # Bulyan: per-round all-reduce of the distance partials (median /
         # trimmed mean), all-reduced Gram (krum), local per-coordinate stage
         c = BULYAN_CASE
@@ -199,6 +215,34 @@ def test_pipelined_cyclic_equals_unsharded(world, two_rank_results, three_rank_r
     for r in range(world):
         for block in (64, 96, 1001):
             np.testing.assert_array_equal(res[r]["cyclic_%d" % block], want)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c5_pipelined_mom_filter_equals_unsharded(world, two_rank_results, three_rank_results):
+    """bench.py's N > 1 path for config C5 (mom_filterl2): itv-aligned
+    block-cyclic shards, the per-block filter, the overlapped all-gather --
+    equal to the unsharded oracle over the whole matrix."""
+    _setup_paths()
+    from oracle import robust_np as orc
+    from synth import make_rows
+    res = two_rank_results if world == 2 else three_rank_results
+    xc5 = make_rows(24, 160 * world, seed=14, byz=4)
+    want = np.asarray(orc.mom_filterL2(list(xc5), 0.2, 0.02, 20, 40, float(np.exp(-2.0)))).ravel()
+    for r in range(world):
+        assert res[r]["c5_block"] == 40
+        np.testing.assert_allclose(res[r]["c5"], want, rtol=1e-12, atol=1e-15)
+
+
+def test_filter_block_is_itv_aligned():
+    _setup_paths()
+    import bench
+    for d, chunks, itv in ((12_500_000, 16, 1000), (10_000_000, 16, 1000), (160, 4, 40), (1000, 16, 1000),
+                           (999, 16, 1000)):
+        b = bench.filter_block(d, chunks, itv)
+        if b:
+            assert d % b == 0 and b % itv == 0 and d // b <= chunks
+        else:
+            assert d % itv != 0
 
 
 def test_shard_bounds_cover_and_align():
