@@ -66,6 +66,21 @@ def test_strided_rows_and_vec4_average():
     np.testing.assert_array_equal(engine.average(sub).cpu().numpy(), orc.average(list(x[:, 5:3005])))
 
 
+def test_expanded_and_overlapping_views_are_copied():
+    """Row stride below d (an expanded 0-stride view, an overlapping
+    as_strided view) must not make the kernels walk past the storage: the
+    engine takes a contiguous copy (engine._unit_rows)."""
+    v = torch.from_numpy(make_rows(1, 3000, seed=4)[0]).cuda()
+    ex = v.expand(64, 3000)
+    assert ex.stride(0) == 0
+    np.testing.assert_array_equal(engine.trimmed_mean(ex).cpu().numpy(), engine.trimmed_mean(ex.contiguous()).cpu().numpy())
+    np.testing.assert_array_equal(engine.median(ex).cpu().numpy(), v.cpu().numpy())
+    base = torch.from_numpy(make_rows(1, 4000, seed=5)[0]).cuda()
+    ov = base.as_strided((32, 3000), (31, 1))          # rows overlap (stride 31 < d)
+    np.testing.assert_array_equal(engine.median(ov).cpu().numpy(), engine.median(ov.contiguous()).cpu().numpy())
+    np.testing.assert_array_equal(engine.average(ov).cpu().numpy(), engine.average(ov.contiguous()).cpu().numpy())
+
+
 def test_c1_convnet_round_bitexact():
     z = np.load(GOLDEN + "/c1_convnet_n100.npz")
     layers = make_convnet_round(int(z["n"]), int(z["seed"]))
