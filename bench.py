@@ -185,8 +185,10 @@ def roofline_model(agg, n, d):
         # chunk Grams (fp64 MFMA) + the client-space solver (fp64), the solver
         # priced from chunk 0's measured Lanczos steps (solver_flops below)
         return "mfma", MFMA64_PEAK_TFLOPS, "TFLOP/s", n * (n + 1) * d
-    # MoM filters: bucket pass (HBM) dominates at C5
-    return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
+    # MoM filters: the same over the B bucket means (the bucket pass itself,
+    # 4Nd + 4Bd bytes, is ~2 % of the call at C5); solver flops added below
+    b = engine.mom_bucket_count(n, FILTER_ARGS["eps"], MOM_DELTA)[0]
+    return "mfma", MFMA64_PEAK_TFLOPS, "TFLOP/s", b * (b + 1) * d
 
 
 def solver_flops(agg, X, itv=1000):
@@ -196,9 +198,12 @@ def solver_flops(agg, X, itv=1000):
     (~3 n_a^2) and every Lanczos step is one symmetric matvec (2 n_a^2) plus
     O(n_a) vector work, n_a = the clients still active.  Chunks are assumed
     to take chunk 0's step counts (they see statistically identical data)."""
-    mode = 0 if agg == "filterl2" else 1
+    mode = 0 if agg in ("filterl2", "mom_filterl2") else 1
     fa = FILTER_ARGS
     Xc = X[:, :itv]
+    if agg.startswith("mom_"):
+        num, size = engine.mom_bucket_count(int(X.shape[0]), fa["eps"], MOM_DELTA)
+        Xc = engine.bucket_means(Xc, size, num)
     _, _, recs = engine.filter_debug(Xc, mode, fa["eps"], fa["sigma"], fa["expansion"], fa["itv"])
     recs = recs.numpy()
     per_chunk = 0.0
@@ -398,11 +403,11 @@ def main():
 
     bound, peak, unit, alg = roofline_model(a.agg, n, d)
     solver_note = None
-    if a.agg in ("filterl2", "ex_noregret"):
+    if a.agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
         sflops, iters = solver_flops(a.agg, X)
         alg = alg + int(sflops)
-        solver_note = "chunk Grams n(n+1)d + solver %.3g flop (chunk 0: %d iterations, its Lanczos steps)" % (
-            sflops, iters)
+        solver_note = "chunk Grams n(n+1)d + solver %.3g flop (chunk 0: %d iterations, its Lanczos steps)%s" % (
+            sflops, iters, ", n = the bucket means" if a.agg.startswith("mom_") else "")
     scale = 1e9 if unit == "GB/s" else 1e12
     achieved = alg / (kern_ms * 1e-3) / scale
     traffic = None
