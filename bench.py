@@ -138,9 +138,11 @@ KERNEL_NAME = {
     "bulyankrum": "whole bulyan op (bf16x3 Gram + theta Krum rounds + final stage)",
     "bulyanmedian": "whole bulyan op (theta fused select+distance rounds + final stage)",
     "bulyantrimmedmean": "whole bulyan op (theta fused select+distance rounds + final stage)",
-    "filterl2": "whole filterL2 op (chunk_gram_kernel fp64 MFMA + filter_solve_kernel<0> + chunk_mean_kernel)",
+    "filterl2": "whole filterL2 op (chunk_gram_kernel fp64 MFMA + lanczos_solve_kernel<0>, listed chunks on "
+                "filter_solve_kernel<0> + chunk_mean_kernel)",
     "ex_noregret": "whole ex_noregret op (chunk Gram + noregret_pre_kernel + filter_solve_kernel<1> + chunk means)",
-    "mom_filterl2": "whole op (bucket means + chunk Gram + filter_solve_kernel<0> + chunk means)",
+    "mom_filterl2": "whole op (bucket means + chunk Gram + lanczos_solve_kernel<0> / filter_solve_kernel<0> "
+                    "fallback + chunk means)",
     "mom_ex_noregret": "whole op (bucket means + chunk Gram + filter_solve_kernel<1> + chunk means)",
 }
 
