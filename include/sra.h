@@ -200,6 +200,22 @@ int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mo
                    double sigma, double expansion, double* out, int32_t* status, void* ws, size_t ws_bytes,
                    void* stream);
 
+/* As sra_filter_f32, and records every chunk's discrete decisions into trace
+ * (device int32, nchunks x SRA_FILTER_TRACE_STRIDE; replaces nothing in the
+ * reference -- it exposes what robust_estimator.py:163-174 / :49-51, :71-99
+ * decide, so tests can pin them):
+ *   [0]            iterations completed (< T when the early exit fired)
+ *   [1 + it]       filterL2: the client removed at iteration it (argmax tau,
+ *                  first index, original numbering); ex_noregret: how many
+ *                  weights the kept KL-projection candidate caps
+ *   [1 + 128 + i]  1 if client i is active at the end (filterL2: not removed;
+ *                  ex_noregret: kept by the Krum pre-filter), else 0
+ * Unused decision slots are left untouched. */
+#define SRA_FILTER_TRACE_STRIDE (1 + 2 * 128)
+int sra_filter_trace_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv, double eps,
+                         double sigma, double expansion, double* out, int32_t* status, int32_t* trace, void* ws,
+                         size_t ws_bytes, void* stream);
+
 /* Diagnostics variant: as sra_filter_f32, and additionally writes chunk 0's
  * centred Gram (128 x 128 fp64, row-major, zero-padded) followed by one record
  * of 144 doubles per filter iteration (weights before the update [128], top

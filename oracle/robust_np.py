@@ -358,20 +358,58 @@ def _weighted_cov(centered, c, order="gemm"):
     return (centered.T * c) @ centered / c.sum()
 
 
-def filterL2_(samples, eps=0.2, sigma=1, expansion=20, order="gemm"):
-    """robust_estimator.py:144-177 on one (n, k) chunk (primal k x k form)."""
+def _top_eig(z, c, order):
+    """Top eigenpair (lambda, unit v) of the weighted covariance of the centred
+    chunk z (robust_estimator.py:158-161).  order "gemm" / "reverse": LAPACK on
+    the k x k covariance (the reference's primal form, two fp64 client orders);
+    "dual": LAPACK on the n x n matrix M = W^1/2 Z Z^T W^1/2 (w = c / sum c),
+    whose nonzero spectrum is the covariance's, v = Z^T W^1/2 u / |.| -- the
+    same mathematics ~100x faster at n = 128, k = 1000, used as the checker of
+    the full-size device traces (tests/test_gpu_filter_trace.py)."""
+    k = z.shape[1]
+    if order in ("dual", "dual_reverse"):
+        # dual_reverse: the same with the clients in reverse order (another
+        # rounding of the same mathematics)
+        n = z.shape[0]
+        p = np.arange(n)[::-1] if order == "dual_reverse" else np.arange(n)
+        sw = np.sqrt(c[p] / c[p].sum())
+        zs = z[p] * sw[:, None]
+        lam, u = eigh(zs @ zs.T, subset_by_index=[n - 1, n - 1])
+        v = z[p].T @ (sw * u[:, 0])
+        return lam[0], v / np.linalg.norm(v)
+    lam, vec = eigh(_weighted_cov(z, c, order), subset_by_index=[k - 1, k - 1])
+    return lam[0], vec[:, 0]
+
+
+def filterL2_(samples, eps=0.2, sigma=1, expansion=20, order="gemm", trace=None):
+    """robust_estimator.py:144-177 on one (n, k) chunk (primal k x k form).
+
+    ``trace``: a list; one record per call is appended -- the decisions the
+    reference makes (:163-174): ``removed`` = the ORIGINAL index of the
+    argmax-tau client dropped at each iteration (first index on ties),
+    ``iters`` = the iterations completed (< T when the early exit of :163-164
+    fired), ``margin`` = (tau_max - tau_2nd) / tau_max per iteration (how
+    close each removal was to a tie)."""
     x = np.asarray(samples)
     n0, k = x.shape
     c = np.ones(n0)
-    for _ in range(2 * int(eps * n0)):
+    alive = list(range(n0))
+    rec = {"removed": [], "margin": [], "iters": 0} if trace is not None else None
+    if rec is not None:
+        trace.append(rec)
+    for it in range(2 * int(eps * n0)):
         mu = np.average(x, axis=0, weights=c)
         z = x - mu
-        lam, vec = eigh(_weighted_cov(z, c, order), subset_by_index=[k - 1, k - 1])
-        lam = lam[0]
+        lam, vec = _top_eig(z, c, order)
         if lam * lam <= expansion * sigma * sigma:
             return mu
-        tau = (z @ vec[:, 0]) ** 2
+        tau = (z @ vec) ** 2
         top = int(np.argmax(tau))
+        if rec is not None:
+            srt = np.sort(tau)
+            rec["removed"].append(alive.pop(top))
+            rec["margin"].append(float((srt[-1] - srt[-2]) / srt[-1]) if len(srt) > 1 else 1.0)
+            rec["iters"] = it + 1
         c = c * (1 - tau / tau[top])
         x = np.delete(x, top, axis=0)
         c = np.delete(c, top)
@@ -388,27 +426,31 @@ def _chunked(samples, itv, fn):
     return np.concatenate(out, axis=0).reshape(shape)
 
 
-def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, order="gemm"):
-    """robust_estimator.py:180-208: filterL2_ over itv-wide chunks."""
-    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion, order))
+def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, order="gemm", trace=None):
+    """robust_estimator.py:180-208: filterL2_ over itv-wide chunks (``trace``:
+    one filterL2_ record per chunk, in chunk order)."""
+    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion, order, trace))
 
 
-def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30), order="gemm"):
-    """robust_estimator.py:210-218."""
+def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30), order="gemm",
+                 trace=None):
+    """robust_estimator.py:210-218 (trace: bucket indices, see filterL2_)."""
     num, size = bucket_count(len(samples), eps, delta)
-    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv, order)
+    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv, order, trace)
 
 
-def kl_capped_projection(c, eps):
+def kl_capped_projection(c, eps, info=None):
     """The projection step of robust_estimator.py:77-99: among the candidates
     that cap the i+1 largest weights at 1/((1-eps)n) and rescale the rest to sum
     to one, keep the feasible one with the smallest KL(c || c_) (first on ties).
     Returns None when no candidate is feasible (the reference then fails on the
-    next iteration)."""
+    next iteration).  ``info`` (a dict): ``capped`` = i+1 of the kept candidate,
+    ``margin`` = relative KL gap to the runner-up (1.0 with a single feasible
+    candidate)."""
     n = len(c)
     cap = 1.0 / (1 - eps) / n
     desc = np.argsort(c)[::-1]
-    best, best_kl = None, None
+    best, best_kl, best_i, kls = None, None, -1, []
     for i in range(n):
         head, tail = desc[:i + 1], desc[i + 1:]
         cand = c.copy()
@@ -421,18 +463,32 @@ def kl_capped_projection(c, eps):
         if cand[tail[0]] > cap:
             continue
         kl = rel_entr(c, cand).sum()
+        kls.append(kl)
         if best_kl is None or kl < best_kl:
-            best, best_kl = cand, kl
+            best, best_kl, best_i = cand, kl, i
+    if info is not None:
+        info["capped"] = best_i + 1
+        srt = np.sort(kls)
+        info["margin"] = float((srt[1] - srt[0]) / max(abs(srt[0]), 1e-300)) if len(srt) > 1 else 1.0
     return best
 
 
-def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7):
-    """robust_estimator.py:42-102 on one (n, k) chunk."""
+def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7, trace=None, order="gemm"):
+    """robust_estimator.py:42-102 on one (n, k) chunk.  ``trace``: a list; one
+    record per call is appended -- ``kept`` = the clients the Krum pre-filter
+    keeps (:49-51, ascending original indices), ``capped`` = how many weights
+    the chosen KL projection candidate caps at each iteration (:78-99),
+    ``iters`` = the iterations completed (< T on the early exit :71-72),
+    ``margin`` = the candidate's relative KL gap to the runner-up."""
     x = np.asarray(samples)
     n = len(x)
     f = int(np.ceil(eps * n))
     scores = krum_(list(x), f)
     keep = np.argpartition(scores, -f)[:-f]
+    rec = None
+    if trace is not None:
+        rec = {"kept": sorted(int(i) for i in keep), "capped": [], "margin": [], "iters": 0}
+        trace.append(rec)
     x = x[keep]
     m, k = x.shape
     if m < 2:
@@ -442,30 +498,75 @@ def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7)
     far = pairwise_l2(list(x))
     step = 0.5 / (np.amax(far[np.triu_indices(m, 1)]) ** 2)
     c = np.ones(m)
-    for _ in range(int(2 * eps * m)):
+    for it in range(int(2 * eps * m)):
         mu = np.average(x, axis=0, weights=c)
         z = x - mu
-        lam, vec = eigh(_weighted_cov(z, c), subset_by_index=[k - 1, k - 1])
-        lam = lam[0]
+        lam, vec = _top_eig(z, c, order)
         if lam * lam <= expansion * sigma * sigma:
             return mu
-        tau = (z @ vec[:, 0]) ** 2
+        tau = (z @ vec) ** 2
         c = c * (1 - step * tau)
-        c = kl_capped_projection(c, eps)
+        info = {}
+        c = kl_capped_projection(c, eps, info)
+        if rec is not None:
+            rec["capped"].append(info["capped"])
+            rec["margin"].append(info["margin"])
+            rec["iters"] = it + 1
         if c is None:
             raise TypeError("ex_noregret: no feasible capped-simplex projection")
     return np.average(x, axis=0, weights=c)
 
 
-def ex_noregret(samples, eps=1. / 12, sigma=1, expansion=20, itv=ITV):
+def ex_noregret(samples, eps=1. / 12, sigma=1, expansion=20, itv=ITV, trace=None, order="gemm"):
     """robust_estimator.py:104-133: ex_noregret_ over itv-wide chunks."""
-    return _chunked(samples, itv, lambda ch: ex_noregret_(ch, eps, sigma, expansion))
+    return _chunked(samples, itv, lambda ch: ex_noregret_(ch, eps, sigma, expansion, trace=trace, order=order))
 
 
-def mom_ex_noregret(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
+def mom_ex_noregret(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30), trace=None,
+                    order="gemm"):
     """robust_estimator.py:135-142."""
     num, size = bucket_count(len(samples), eps, delta)
-    return ex_noregret(bucket_means(samples, size, num), eps, sigma, expansion, itv)
+    return ex_noregret(bucket_means(samples, size, num), eps, sigma, expansion, itv, trace, order)
+
+
+def trace_pair(args):
+    """Test helper (picklable for a process pool): the decision traces of one
+    (n, k) chunk from the client-space oracle in two client orders ("dual",
+    "dual_reverse").  args = (x, mode, eps, sigma, expansion); returns two
+    rows [iters, decision(n), active flag(n)] (trace_array layout + flags)."""
+    x, mode, eps, sigma, expansion = args
+    rows = []
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for order in ("dual", "dual_reverse"):
+            tr = []
+            if mode == 0:
+                filterL2_(x, eps, sigma, expansion, order=order, trace=tr)
+            else:
+                ex_noregret_(x, eps, sigma, expansion, trace=tr, order=order)
+            n = x.shape[0]
+            flags = np.zeros(n, np.int32)
+            if mode == 0:
+                flags[:] = 1
+                flags[tr[0]["removed"]] = 0
+            else:
+                flags[tr[0]["kept"]] = 1
+            rows.append(np.concatenate([trace_array(tr, mode, n)[0], flags]))
+    return rows
+
+
+def trace_array(records, mode, n):
+    """Pack per-chunk filter traces into the engine's int32 layout
+    (sra_filter_trace_f32): row = [iters, decision_0 .. decision_{T-1}, -1 pad]
+    with decision = the removed client (filterL2) or the capped count
+    (ex_noregret), T = 2 * int(eps * n) resp. int(2 * eps * n_kept) <= n."""
+    out = np.full((len(records), 1 + n), -1, dtype=np.int32)
+    for i, r in enumerate(records):
+        dec = r["removed"] if mode == 0 else r["capped"]
+        out[i, 0] = r["iters"]
+        out[i, 1:1 + len(dec)] = dec
+    return out
 
 
 # ----------------------------------------------------------------------------

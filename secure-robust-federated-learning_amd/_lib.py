@@ -81,6 +81,8 @@ _SIGS = {
     "sra_bulyan_stage_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr, _sz, _ptr],
     "sra_filter_workspace_bytes": [_i64, _i64, _i32, ctypes.POINTER(_sz)],
     "sra_filter_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _dbl, _dbl, _dbl, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_filter_trace_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _dbl, _dbl, _dbl, _ptr, _ptr, _ptr, _ptr, _sz,
+                             _ptr],
     "sra_filter_debug_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _dbl, _dbl, _dbl, _ptr, _ptr, _ptr, _ptr, _sz,
                              _ptr],
     "sra_window_mean_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _i32, _ptr, _i64, _ptr],

@@ -377,7 +377,16 @@ struct SolveArgs {
   double* Vg;        // lanczos_solve_kernel: [grid][MMAX][FNP] Lanczos basis per workgroup
   int* fb_list;      // chunks handed to the re-orthogonalising fallback
   int* fb_count;
+  int* trace;        // optional [nb][1 + 2 FNP] decision trace (sra_filter_trace_f32), batch-relative
 };
+
+// Decision trace of one chunk (sra_filter_trace_f32): [0] iterations completed
+// (< T after the early exit), [1 + it] the decision of iteration it -- the
+// removed client (filterL2, robust_estimator.py:166-172) or the capped count of
+// the kept projection candidate (ex_noregret, :78-99) -- and [1 + FNP + row]
+// whether the client is still active at the end (ex_noregret: kept by the
+// Krum pre-filter, :49-51).
+constexpr int kTraceStride = 1 + 2 * FNP;
 
 constexpr size_t kSolveLds =
     sizeof(double) * (static_cast<size_t>(LMAX) * VST + 2 * XLEN + 64 + 32 + 4 * TRI + 4 * FNP) +
@@ -540,7 +549,7 @@ __device__ __attribute__((noinline)) void tri_top(double* trw, int m, double tsc
 // candidate is feasible.  Block-wide (all 256 lanes), barriers inside.
 __device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int row, bool own, int nk, double cap,
                                                      double* cvec, double* vscr, int* ibuf, double* red,
-                                                     double* hbuf) {
+                                                     double* hbuf, int* capped) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int* kidx = ibuf;            // compact -> client row
   int* irank = ibuf + FNP;     // descending rank of a compact entry
@@ -621,6 +630,7 @@ __device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int
       bi = islot[4 + q2];
     }
   const bool ok = bv > -__builtin_inf();
+  *capped = ok ? bi + 1 : 0;
   if (ok && tid == bi) hbuf[0] = scale;
   __syncthreads();
   if (ok && tid < nk) cvec[kidx[tid]] = irank[tid] <= bi ? cap : cc[tid] * hbuf[0];
@@ -754,6 +764,8 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
     bool have_u = false;
     int m_hint = 12;          // Lanczos steps the previous iteration needed
     double rate_hint = 0.0;   // last measured log-decay of the Ritz residual per step (0: none yet)
+    int done = 0;             // filter iterations completed (decision trace)
+    int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
 
     for (int it = 0; it < iters; ++it) {
       const long long t_it = dbg ? clock64() : 0;
@@ -1000,17 +1012,25 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
         reduce4(own ? fabs(cn) : 0.0, 0.0, 0.0, 0.0, o, 1);
         ci = cn / o[0];
         if (row == p) ai = false;
+        if (tr != nullptr && tid == 0) tr[1 + it] = p;
       } else {
         // c *= 1 - step*tau, then the KL projection onto {sum c = 1, c <= cap}
         // (robust_estimator.py:74-99) over the n_keep kept clients
         const int nk = n_keep;
         const double cap = 1.0 / (1.0 - A.eps) / nk;
         if (ai) ci = ci * (1.0 - step * ti);
-        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf)) {
+        int capped = 0;
+        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf, &capped)) {
           if (tid == 0) *A.status = 2;   // projected_c None -> TypeError in the reference
           break;
         }
+        if (tr != nullptr && tid == 0) tr[1 + it] = capped;
       }
+      done = it + 1;
+    }
+    if (tr != nullptr) {
+      if (tid == 0) tr[0] = done;
+      if (own) tr[1 + FNP + row] = ai ? 1 : 0;
     }
 
     // ---- final weights and np.average's scale (pairwise sum of the kept weights in order)
@@ -1373,6 +1393,8 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
     int m_hint = 24;
     double rate_hint = 0.0;
     bool fallback = false;
+    int done = 0;   // filter iterations completed (decision trace)
+    int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
     int clog_n = 0;   // DBG: checks logged (per chunk, last 60 kept from the start)
 
     for (int it = 0; it < iters; ++it) {
@@ -1589,15 +1611,19 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         reduce4(own ? fabs(cn) : 0.0, 0.0, o, 1);
         ci = cn / o[0];
         if (row == p) ai = false;
+        if (tr != nullptr && tid == 0) tr[1 + it] = p;
       } else {
         const int nk = n_keep;
         const double cap = 1.0 / (1.0 - A.eps) / nk;
         if (ai) ci = ci * (1.0 - step * ti);
-        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf)) {
+        int capped = 0;
+        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf, &capped)) {
           if (tid == 0) *A.status = 2;
           break;
         }
+        if (tr != nullptr && tid == 0) tr[1 + it] = capped;
       }
+      done = it + 1;
       __syncthreads();   // every wave's gmv reads of xbuf before the next iteration writes it
     }
 
@@ -1618,7 +1644,9 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       ibuf[2 * FNP + row] = ai ? 1 : 0;
       A.c[static_cast<size_t>(ch) * FNP + row] = ai ? ci : 0.0;
       A.act[static_cast<size_t>(ch) * FNP + row] = ai ? 1 : 0;
+      if (tr != nullptr) tr[1 + FNP + row] = ai ? 1 : 0;
     }
+    if (tr != nullptr && tid == 0) tr[0] = done;
     __syncthreads();
     if (tid == 0) {
       int q2 = 0;
@@ -1673,7 +1701,7 @@ size_t filter_workspace_bytes(int64_t d, int itv) {
 }
 
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
-                  double expansion, double* out, int* status, double* dbg, void* ws, size_t ws_bytes,
+                  double expansion, double* out, int* status, double* dbg, int* trace, void* ws, size_t ws_bytes,
                   hipStream_t s) {
   SRA_REQUIRE(n >= 1 && n <= FNP, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", FNP, n);
   SRA_REQUIRE(itv >= 1, SRA_ERR_ARG, "itv must be >= 1");
@@ -1713,7 +1741,8 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("noregret_pre_kernel");
       if (rc) return rc;
     }
-    SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc};
+    SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
+                 trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr};
     SRA_HIP(hipMemsetAsync(fbc, 0, 4 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
     if (mode == 1) {
@@ -1783,7 +1812,17 @@ extern "C" int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx,
   const int rc = sra::filter_checks(X, n, d, ldx, mode, eps, out, status);
   if (rc) return rc;
   return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, nullptr,
-                            ws, ws_bytes, static_cast<hipStream_t>(stream));
+                            nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_filter_trace_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
+                                    double eps, double sigma, double expansion, double* out, int32_t* status,
+                                    int32_t* trace, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(trace != nullptr, SRA_ERR_ARG, "null trace pointer");
+  const int rc = sra::filter_checks(X, n, d, ldx, mode, eps, out, status);
+  if (rc) return rc;
+  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, nullptr,
+                            trace, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
@@ -1792,6 +1831,6 @@ extern "C" int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_
   SRA_REQUIRE(dbg != nullptr, SRA_ERR_ARG, "null pointer");
   const int rc = sra::filter_checks(X, n, d, ldx, mode, eps, out, status);
   if (rc) return rc;
-  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, dbg, ws,
-                            ws_bytes, static_cast<hipStream_t>(stream));
+  return sra::launch_filter(mode, X, static_cast<int>(n), d, ldx, itv, eps, sigma, expansion, out, status, dbg,
+                            nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }

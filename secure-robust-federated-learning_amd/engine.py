@@ -10,6 +10,7 @@ per function).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -261,6 +262,29 @@ def _filter(X, mode, eps, sigma, expansion, itv, check):
     if check and int(status.item()) == 2:
         raise TypeError("ex_noregret: no feasible capped-simplex projection (projected_c is None)")
     return out
+
+
+FILTER_TRACE_STRIDE = 1 + 2 * 128
+
+
+def filter_trace(X, mode, eps, sigma, expansion, itv):
+    """Run a filter (mode 0 filterL2, 1 ex_noregret) and return (out, trace):
+    trace is a host int32 (nchunks, 1 + 2n) array [iterations completed,
+    decision per iteration (-1 unused), active flag per client] -- the layout
+    of oracle.robust_np.trace_array (sra_filter_trace_f32, include/sra.h)."""
+    X, n, d, ldx = as_matrix(X)
+    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    status = torch.zeros(1, dtype=torch.int32, device=X.device)
+    w = chunk_width(d, itv)
+    nch = -(-d // w)
+    tr = torch.full((nch, FILTER_TRACE_STRIDE), -1, dtype=torch.int32, device=X.device)
+    nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_filter_trace_f32", X.data_ptr(), n, d, ldx, int(mode), w, float(eps), float(sigma),
+              float(expansion), out.data_ptr(), status.data_ptr(), tr.data_ptr(), ws.data_ptr(), nb,
+              _stream_ptr(X.device))
+    tr = tr.cpu().numpy()
+    return out, np.concatenate([tr[:, :1 + n], tr[:, 1 + 128:1 + 128 + n]], axis=1)
 
 
 FILTER_DEBUG_DOUBLES = 128 * 128 + 256 * 144

@@ -53,7 +53,7 @@ def load_fixture(path):
 def fixtures(prefix=None, func=None):
     out = []
     for p in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
-        if os.path.basename(p).startswith(("c1_", "dispatch_", "attack_", "dba_", "bulyan_coord")):
+        if os.path.basename(p).startswith(("c1_", "dispatch_", "attack_", "dba_", "bulyan_coord", "trace_")):
             continue
         rec = load_fixture(p)
         if prefix and not rec["name"].startswith(prefix):
@@ -67,3 +67,29 @@ def fixtures(prefix=None, func=None):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+def trace_fixtures():
+    """The filter decision-trace fixtures (tests/golden/gen_filter_traces.py +
+    add_trace_bounds.py)."""
+    return [load_fixture(p) for p in sorted(glob.glob(os.path.join(GOLDEN, "trace_*.npz")))]
+
+
+# the C4 / C5 output fixtures share their inputs with these trace fixtures,
+# whose per-chunk bounds (add_trace_bounds.py) then apply to them as well
+TRACE_OF = {"filterL2_n128_c4": "trace_filterL2_c4", "ex_noregret_n128_c4": "trace_ex_noregret_c4",
+            "mom_filterL2_n512_c5": "trace_mom_filterL2_c5"}
+
+
+def assert_chunks_within_bound(got, rec):
+    """got vs rec["out"] chunk by chunk within the matching trace fixture's
+    bound (relative to each chunk's max|out|)."""
+    t = load_fixture(os.path.join(GOLDEN, TRACE_OF[rec["name"]] + ".npz"))
+    np.testing.assert_array_equal(t["x"].reshape(t["x"].shape[0], -1), rec["x"].reshape(rec["x"].shape[0], -1))
+    want = rec["out"].ravel()
+    got = np.asarray(got).ravel()
+    itv = t["params"]["itv"]
+    for c, b in enumerate(t["bound"]):
+        sl = slice(c * itv, (c + 1) * itv)
+        err = np.abs(got[sl] - want[sl]).max() / np.abs(want[sl]).max()
+        assert err <= b, "%s chunk %d: %.3e of max > bound %.3e" % (rec["name"], c, err, b)

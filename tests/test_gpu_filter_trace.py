@@ -1,0 +1,135 @@
+"""GPU: the spectral filters make the reference's discrete decisions.
+
+filterL2_ (robust_estimator.py:144-177) removes the argmax-tau client every
+iteration and may exit early; ex_noregret_ (:42-102) keeps the Krum
+pre-filter's clients and chooses one capped-simplex candidate per iteration.
+These decisions are the exact parity of a chaotic fp64 iteration (the output
+itself moves 1e-6 .. 1e-2 of max under rounding), so they are
+pinned here through sra_filter_trace_f32:
+
+* trace fixtures (tests/golden/trace_*.npz, recorded from the LIVE reference
+  by gen_filter_traces.py): the device makes the reference's decision at every
+  iteration of the agreed prefix (where three independent fp64 oracle
+  evaluations all agree with the reference, add_trace_bounds.py -- every
+  iteration of every chunk but the last one of trace_mom_filterL2_bench chunk
+  0), has the same iteration count and final active set where the whole trace
+  is agreed, and lands within the chunk's bound (3x the farthest oracle
+  evaluation from the reference);
+* full size (C4 N=128 x d=1e7, C5 per GPU N=512 x d=1.25e7): 24 chunks
+  (first, last, random) against the oracle's client-space evaluation in two
+  client orders ("dual", "dual_reverse"), on the prefix where those two agree.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available, trace_fixtures
+from oracle import robust_np as orc
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+    from srfl_amd import engine
+
+TRACES = trace_fixtures()
+SIM = dict(eps=0.2, sigma=1e-5, expansion=20, itv=1000)
+MODE = {"filterL2": 0, "mom_filterL2": 0, "ex_noregret": 1}
+
+
+def _device_trace(func, x, p):
+    X = torch.from_numpy(np.ascontiguousarray(x.reshape(x.shape[0], -1))).cuda()
+    if func == "mom_filterL2":
+        num, size = engine.mom_bucket_count(X.shape[0], p["eps"], p["delta"])
+        X = engine.bucket_means(X, size, num)
+    out, tr = engine.filter_trace(X, MODE[func], p["eps"], p["sigma"], p["expansion"], p["itv"])
+    return out.cpu().numpy(), tr
+
+
+def _check_prefix(got, want, agree, n, what):
+    """got / want: one chunk's [iters, decisions(n), flags(n)]."""
+    a = int(agree)
+    np.testing.assert_array_equal(got[1:1 + a], want[1:1 + a], err_msg="%s: decisions differ" % what)
+    if a == int(want[0]):
+        assert got[0] == want[0], "%s: iterations %d vs %d" % (what, got[0], want[0])
+        np.testing.assert_array_equal(got[1 + n:1 + 2 * n], want[1 + n:1 + 2 * n],
+                                      err_msg="%s: final active set differs" % what)
+
+
+@pytest.mark.parametrize("rec", TRACES, ids=[r["name"] for r in TRACES])
+def test_trace_matches_reference(rec):
+    p, func = rec["params"], rec["func"]
+    out, tr = _device_trace(func, rec["x"], p)
+    want = rec["trace"]
+    n = want.shape[1] // 2
+    assert tr.shape == want.shape
+    errs = []
+    for c in range(want.shape[0]):
+        _check_prefix(tr[c], want[c], rec["agree"][c], n, "%s chunk %d" % (rec["name"], c))
+        sl = slice(c * p["itv"], (c + 1) * p["itv"])
+        m = np.abs(rec["out"][sl]).max()
+        err = np.abs(out[sl] - rec["out"][sl]).max() / m
+        errs.append(err / rec["bound"][c])
+        assert err <= rec["bound"][c], "%s chunk %d: %.3e of max > bound %.3e" % (
+            rec["name"], c, err, rec["bound"][c])
+    print("%s: error / bound per chunk %s" % (rec["name"], ["%.3f" % e for e in errs]))
+
+
+def _device_rows(n, d, byz, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    X = torch.empty((n, d), dtype=torch.float32, device="cuda")
+    drift = torch.empty(d, dtype=torch.float32, device="cuda").normal_(0, 0.001, generator=g)
+    for r0 in range(0, n, 16):
+        X[r0:r0 + 16].normal_(0, 0.01, generator=g).add_(drift)
+    if byz:
+        mean = X[byz:].double().mean(0)
+        X[:byz] = (-10.0 * mean).float()[None, :] + 0.001 * torch.randn(byz, d, device="cuda", generator=g)
+    return X
+
+
+def _fullsize(X, mode, nsample=24, seed=0):
+    out, tr = engine.filter_trace(X, mode, SIM["eps"], SIM["sigma"], SIM["expansion"], SIM["itv"])
+    n, d = X.shape
+    nch = -(-d // SIM["itv"])
+    rng = np.random.default_rng(seed)
+    chunks = sorted({0, nch - 1, *rng.choice(nch, nsample - 2, replace=False).tolist()})
+    args = [(X[:, c * 1000:(c + 1) * 1000].cpu().numpy(), mode, SIM["eps"], SIM["sigma"], SIM["expansion"])
+            for c in chunks]
+    with mp.get_context("spawn").Pool(min(8, len(args))) as pool:
+        refs = pool.map(orc.trace_pair, args)
+    agreed = 0
+    for c, (a, b) in zip(chunks, refs):
+        diff = np.nonzero(a[1:1 + a[0]] != b[1:1 + a[0]])[0]
+        agree = int(diff[0]) if diff.size else (int(a[0]) if a[0] == b[0] else int(min(a[0], b[0])))
+        agreed += agree == a[0]
+        _check_prefix(tr[c], a, agree, n, "chunk %d" % c)
+        if mode == 1:   # the Krum pre-filter's kept set
+            np.testing.assert_array_equal(tr[c, 1 + n:], a[1 + n:], err_msg="chunk %d: kept set" % c)
+    assert np.isfinite(out.cpu().numpy()).all()
+    assert agreed >= len(chunks) // 2
+    return agreed, len(chunks)
+
+
+def test_c4_filterl2_fullsize_trace():
+    X = _device_rows(128, 10_000_000, 20, seed=41)
+    agreed, total = _fullsize(X, 0)
+    print("C4 filterL2: %d of %d sampled chunks fully agreed" % (agreed, total))
+
+
+def test_c4_ex_noregret_fullsize_trace():
+    X = _device_rows(128, 10_000_000, 20, seed=42)
+    agreed, total = _fullsize(X, 1)
+    print("C4 ex_noregret: %d of %d sampled chunks fully agreed" % (agreed, total))
+
+
+def test_c5_mom_filterl2_fullsize_trace():
+    X = _device_rows(512, 12_500_000, 100, seed=43)
+    num, size = engine.mom_bucket_count(512, SIM["eps"], float(np.exp(-26)))
+    B = engine.bucket_means(X, size, num)
+    del X
+    agreed, total = _fullsize(B, 0)
+    print("C5 mom_filterL2: %d of %d sampled chunks fully agreed" % (agreed, total))

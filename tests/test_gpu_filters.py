@@ -15,8 +15,7 @@ import warnings
 import numpy as np
 import pytest
 
-from conftest import fixtures, gpu_available
-from test_oracle_golden import FILTER_C4_ATOL
+from conftest import fixtures, gpu_available, TRACE_OF, assert_chunks_within_bound
 from oracle import robust_np as orc
 from synth import make_rows
 
@@ -51,10 +50,13 @@ def test_golden_filters(rec):
     got = call(xs, rec["params"])
     assert got.dtype == np.float64 and got.shape == rec["out"].shape
     rtol, atol = TOL[rec["func"]]
-    if rec["func"] in ("filterL2", "mom_filterL2") and rec["name"].endswith(("_c4", "_c5")):
-        # the reference's own fp64 error amplification over 50 iterations
-        # (tests/test_oracle_golden.py, FILTER_C4_ATOL)
-        rtol, atol = 0.0, FILTER_C4_ATOL * np.abs(rec["out"]).max()
+    if rec["name"] in TRACE_OF:
+        # C4 / C5: 50 chaotic iterations -- the per-chunk bound of the matching
+        # trace fixture (3x the farthest independent oracle evaluation from the
+        # reference, tests/golden/add_trace_bounds.py); the decisions themselves
+        # are pinned exactly in tests/test_gpu_filter_trace.py
+        assert_chunks_within_bound(got, rec)
+        return
     np.testing.assert_allclose(got, rec["out"], rtol=rtol, atol=atol)
 
 
@@ -90,8 +92,7 @@ def test_filter_chunks_independent_and_full_size_smoke():
     out = engine.filter_l2(Y, 0.2, 1e-5, 20, 1000).cpu().numpy()
     assert np.isfinite(out).all()
     # benign-only data: the hardest case for the eigensolver (clustered spectrum)
-    _chunk_check(Y, out, [999], lambda xs: orc.filterL2(xs, 0.2, 1e-5, 20, 1000), FILTER_C4_ATOL,
-                 lambda xs: orc.filterL2(xs, 0.2, 1e-5, 20, 1000, order="reverse"))
+    _chunk_check(Y, out, [999], lambda xs, o: orc.filterL2(xs, 0.2, 1e-5, 20, 1000, order=o))
 
 
 def test_filter_internals_chunk0():
@@ -133,20 +134,26 @@ def _device_rows(n, d, byz, seed):
     return X
 
 
-def _chunk_check(X, got, chunks, oracle_fn, atol_of_max, spread_fn=None):
-    """Device result on whole chunks vs the oracle.  filterL2's 50 iterations
-    amplify rounding: with ``spread_fn`` the bound also admits
-    10x the distance between two fp64 evaluation orders of the oracle itself
-    (how far the reference's own output moves under rounding on that chunk)."""
+def _chunk_check(X, got, chunks, oracle_fn, orders=("gemm", "reverse", "dual"), floor=0.0):
+    """Device result on whole chunks vs the oracle's first evaluation order.
+    filterL2's 50 iterations carry rounding to 1e-6 .. 1e-2 of max|out|
+    (DESIGN.md §4), so the bound is 3x the farthest of the oracle's other
+    independent fp64 evaluations from the first one (the rule of
+    tests/golden/add_trace_bounds.py, with the oracle standing in for the
+    reference at full size), relative to the chunk's max|out|; ``floor`` is a
+    relative lower bound (ex_noregret's fp32 step, add_trace_bounds.py)."""
     for c in chunks:
         lo, hi = c * 1000, min((c + 1) * 1000, X.shape[1])
         xs = list(X[:, lo:hi].cpu().numpy())
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
-            want = oracle_fn(xs)
-            spread = np.abs(spread_fn(xs) - want).max() if spread_fn is not None else 0.0
-        atol = max(atol_of_max * np.abs(want).max(), 10.0 * spread)
-        np.testing.assert_allclose(got[lo:hi], want, rtol=0, atol=atol)
+            outs = [oracle_fn(xs, o) for o in orders]
+        m = np.abs(outs[0]).max()
+        spread = max([np.abs(o - outs[0]).max() for o in outs[1:]] + [0.0]) / m
+        bound = max(3.0 * spread, floor)
+        err = np.abs(got[lo:hi] - outs[0]).max() / m
+        print("chunk %d: error %.2e of max, bound %.2e" % (c, err, bound))
+        assert err <= bound, "chunk %d: %.3e of max > bound %.3e" % (c, err, bound)
 
 
 def test_c4_filterl2_fullsize_chunks():
@@ -154,8 +161,7 @@ def test_c4_filterl2_fullsize_chunks():
     X = _device_rows(128, 10_000_000, 20, seed=41)
     got = engine.filter_l2(X, **SIM).cpu().numpy()
     assert np.isfinite(got).all()
-    _chunk_check(X, got, [0, 4321, 9999], lambda xs: orc.filterL2(xs, **SIM), FILTER_C4_ATOL,
-                 lambda xs: orc.filterL2(xs, order="reverse", **SIM))
+    _chunk_check(X, got, [0, 4321, 9999], lambda xs, o: orc.filterL2(xs, order=o, **SIM))
 
 
 def test_c4_ex_noregret_fullsize_chunks():
@@ -163,7 +169,7 @@ def test_c4_ex_noregret_fullsize_chunks():
     X = _device_rows(128, 10_000_000, 20, seed=42)
     got = engine.ex_noregret(X, **SIM).cpu().numpy()
     assert np.isfinite(got).all()
-    _chunk_check(X, got, [0, 5678, 9999], lambda xs: orc.ex_noregret(xs, **SIM), 2e-5)
+    _chunk_check(X, got, [0, 5678, 9999], lambda xs, o: orc.ex_noregret(xs, order=o, **SIM), ("dual",), 2e-5)
 
 
 def test_c5_mom_filterl2_per_gpu_shard_chunks():
@@ -173,5 +179,4 @@ def test_c5_mom_filterl2_per_gpu_shard_chunks():
     X = _device_rows(512, 12_500_000, 100, seed=43)
     got = engine.mom_filter_l2(X, delta=delta, **SIM).cpu().numpy()
     assert np.isfinite(got).all()
-    _chunk_check(X, got, [0, 12499], lambda xs: orc.mom_filterL2(xs, delta=delta, **SIM), FILTER_C4_ATOL,
-                 lambda xs: orc.mom_filterL2(xs, delta=delta, order="reverse", **SIM))
+    _chunk_check(X, got, [0, 12499], lambda xs, o: orc.mom_filterL2(xs, delta=delta, order=o, **SIM))

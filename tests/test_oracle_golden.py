@@ -15,7 +15,7 @@ import warnings
 import numpy as np
 import pytest
 
-from conftest import fixtures, GOLDEN
+from conftest import fixtures, GOLDEN, TRACE_OF, assert_chunks_within_bound
 from oracle import robust_np as orc
 from synth import make_convnet_round
 
@@ -32,7 +32,6 @@ CALL = {
     "mom_ex_noregret": lambda xs, p: orc.mom_ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"], p["delta"]),
 }
 EXACT = {"median", "trimmed_mean", "krum", "krum_", "mom_krum", "bulyan"}
-FILTER_C4_ATOL = 1e-3   # of max|out|: see test_oracle_matches_reference
 
 CASES = fixtures()
 
@@ -60,14 +59,12 @@ def test_oracle_matches_reference(rec):
         np.testing.assert_array_equal(got, want)
         if rec["func"] != "krum_":
             assert got.dtype == want.dtype
-    elif rec["func"] in ("filterL2", "mom_filterL2") and rec["name"].endswith(("_c4", "_c5")):
-        # 2*int(eps*N) = 50 iterations, 30 of them on benign clients only: the
-        # reweighting c *= 1 - tau/tau_max amplifies fp64 rounding ~1.3-1.5x per
-        # iteration, so two fp64 evaluations of the reference's own algorithm
-        # (outer-product vs GEMM covariance, identical removal decisions) end
-        # 7.8e-7 (chunk 0) and 2.0e-4 (chunk 1) of max|out| apart (measured,
-        # tools/c4_sensitivity.py); the bound is stated relative to max|out|
-        np.testing.assert_allclose(got, want, rtol=0, atol=FILTER_C4_ATOL * np.abs(want).max())
+    elif rec["name"] in TRACE_OF:
+        # 50 iterations, 30 of them on benign clients only: the reweighting
+        # c *= 1 - tau/tau_max carries fp64 rounding to 1e-6 .. 1e-3 of max|out|
+        # with identical decisions; per-chunk bound = 3x the farthest of three
+        # independent oracle evaluations (tests/golden/add_trace_bounds.py)
+        assert_chunks_within_bound(got, rec)
     else:
         np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
 

@@ -34,6 +34,17 @@ __global__ void kern(float* out, unsigned long long* clk, float k) {
   if constexpr (W == 4) { BODY3("v_med3_f32") }
   if constexpr (W == 5) { BODY("v_min_i32") }
   if constexpr (W == 6) { BODY3("v_maximum3_f32") }
+  if constexpr (W == 7) {   // fp64 FMA (the spectral-filter solver's matvec)
+    double d0 = a0, d1 = a1, d2 = a2, d3 = a3, d4 = a4, d5 = a5, d6 = a6, d7 = a7, dk = k;
+    for (int it = 0; it < ITER; ++it) {
+      asm volatile("v_fma_f64 %0, %0, %8, %8\nv_fma_f64 %1, %1, %8, %8\nv_fma_f64 %2, %2, %8, %8\nv_fma_f64 %3, %3, %8, %8\n"
+                   "v_fma_f64 %4, %4, %8, %8\nv_fma_f64 %5, %5, %8, %8\nv_fma_f64 %6, %6, %8, %8\nv_fma_f64 %7, %7, %8, %8\n"
+                   "v_fma_f64 %0, %0, %8, %8\nv_fma_f64 %1, %1, %8, %8\nv_fma_f64 %2, %2, %8, %8\nv_fma_f64 %3, %3, %8, %8\n"
+                   "v_fma_f64 %4, %4, %8, %8\nv_fma_f64 %5, %5, %8, %8\nv_fma_f64 %6, %6, %8, %8\nv_fma_f64 %7, %7, %8, %8\n"
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7) : "v"(dk));
+    }
+    a0 = (float)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7);
+  }
   unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
   if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
@@ -71,6 +82,7 @@ int main() {
     run<3>("v_min3_f32", w);
     run<4>("v_med3_f32", w);
     run<5>("v_min_i32", w);
+    run<7>("v_fma_f64", w);
   }
   return 0;
 }
