@@ -381,7 +381,17 @@ def _top_eig(z, c, order):
     return lam[0], vec[:, 0]
 
 
-def filterL2_(samples, eps=0.2, sigma=1, expansion=20, order="gemm", trace=None):
+def _perturbed(c, perturb, it):
+    """Test helper: c * (1 + scale * N(0,1)) with a per-(seed, iteration)
+    stream -- a rounding-sized nudge of the weights, used to find which
+    decisions of a chunk are robust to the rounding of an implementation."""
+    if perturb is None:
+        return c
+    seed, scale = perturb
+    return c * (1.0 + scale * np.random.default_rng((seed, it)).standard_normal(c.shape))
+
+
+def filterL2_(samples, eps=0.2, sigma=1, expansion=20, order="gemm", trace=None, perturb=None):
     """robust_estimator.py:144-177 on one (n, k) chunk (primal k x k form).
 
     ``trace``: a list; one record per call is appended -- the decisions the
@@ -398,6 +408,7 @@ def filterL2_(samples, eps=0.2, sigma=1, expansion=20, order="gemm", trace=None)
     if rec is not None:
         trace.append(rec)
     for it in range(2 * int(eps * n0)):
+        c = _perturbed(c, perturb, it)
         mu = np.average(x, axis=0, weights=c)
         z = x - mu
         lam, vec = _top_eig(z, c, order)
@@ -426,17 +437,17 @@ def _chunked(samples, itv, fn):
     return np.concatenate(out, axis=0).reshape(shape)
 
 
-def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, order="gemm", trace=None):
+def filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, order="gemm", trace=None, perturb=None):
     """robust_estimator.py:180-208: filterL2_ over itv-wide chunks (``trace``:
     one filterL2_ record per chunk, in chunk order)."""
-    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion, order, trace))
+    return _chunked(samples, itv, lambda ch: filterL2_(ch, eps, sigma, expansion, order, trace, perturb))
 
 
 def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30), order="gemm",
-                 trace=None):
+                 trace=None, perturb=None):
     """robust_estimator.py:210-218 (trace: bucket indices, see filterL2_)."""
     num, size = bucket_count(len(samples), eps, delta)
-    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv, order, trace)
+    return filterL2(bucket_means(samples, size, num), eps, sigma, expansion, itv, order, trace, perturb)
 
 
 def kl_capped_projection(c, eps, info=None):
@@ -473,7 +484,8 @@ def kl_capped_projection(c, eps, info=None):
     return best
 
 
-def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7, trace=None, order="gemm"):
+def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7, trace=None, order="gemm",
+                 perturb=None):
     """robust_estimator.py:42-102 on one (n, k) chunk.  ``trace``: a list; one
     record per call is appended -- ``kept`` = the clients the Krum pre-filter
     keeps (:49-51, ascending original indices), ``capped`` = how many weights
@@ -499,6 +511,7 @@ def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7,
     step = 0.5 / (np.amax(far[np.triu_indices(m, 1)]) ** 2)
     c = np.ones(m)
     for it in range(int(2 * eps * m)):
+        c = _perturbed(c, perturb, it)
         mu = np.average(x, axis=0, weights=c)
         z = x - mu
         lam, vec = _top_eig(z, c, order)
@@ -529,23 +542,33 @@ def mom_ex_noregret(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.e
     return ex_noregret(bucket_means(samples, size, num), eps, sigma, expansion, itv, trace, order)
 
 
+PERTURB_TRIALS = 4
+PERTURB_SCALE = 1e-13
+
+
 def trace_pair(args):
-    """Test helper (picklable for a process pool): the decision traces of one
+    """Test helper (picklable for a process pool): decision traces of one
     (n, k) chunk from the client-space oracle in two client orders ("dual",
-    "dual_reverse").  args = (x, mode, eps, sigma, expansion); returns two
-    rows [iters, decision(n), active flag(n)] (trace_array layout + flags)."""
+    "dual_reverse") and PERTURB_TRIALS runs whose weights are nudged by
+    PERTURB_SCALE relative noise every iteration.  args = (x, mode, eps,
+    sigma, expansion).  Returns (row, agree, margin): row = the "dual" run's
+    [iters, decision(n), active flag(n)] (trace_array layout + flags), agree =
+    the leading iterations on which every run makes the same decision (a
+    decision that a 1e-13 nudge flips is a near-tie decided by rounding), and
+    the "dual" run's per-iteration margins."""
     x, mode, eps, sigma, expansion = args
-    rows = []
     import warnings
+    n = x.shape[0]
+    runs = [("dual", None), ("dual_reverse", None)] + [("dual", (s, PERTURB_SCALE)) for s in range(PERTURB_TRIALS)]
+    rows, margin = [], None
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        for order in ("dual", "dual_reverse"):
+        for order, pt in runs:
             tr = []
             if mode == 0:
-                filterL2_(x, eps, sigma, expansion, order=order, trace=tr)
+                filterL2_(x, eps, sigma, expansion, order=order, trace=tr, perturb=pt)
             else:
-                ex_noregret_(x, eps, sigma, expansion, trace=tr, order=order)
-            n = x.shape[0]
+                ex_noregret_(x, eps, sigma, expansion, trace=tr, order=order, perturb=pt)
             flags = np.zeros(n, np.int32)
             if mode == 0:
                 flags[:] = 1
@@ -553,7 +576,17 @@ def trace_pair(args):
             else:
                 flags[tr[0]["kept"]] = 1
             rows.append(np.concatenate([trace_array(tr, mode, n)[0], flags]))
-    return rows
+            if margin is None:
+                margin = np.array(tr[0]["margin"])
+    a = rows[0]
+    agree = int(a[0])
+    for b in rows[1:]:
+        diff = np.nonzero(a[1:1 + a[0]] != b[1:1 + a[0]])[0]
+        if diff.size:
+            agree = min(agree, int(diff[0]))
+        elif a[0] != b[0]:
+            agree = min(agree, int(min(a[0], b[0])))
+    return a, agree, margin
 
 
 def trace_array(records, mode, n):

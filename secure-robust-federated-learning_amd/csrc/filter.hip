@@ -1287,21 +1287,383 @@ __device__ __attribute__((noinline)) void block_check(const double* T, int m, do
   *rounds_out = round + 1;
 }
 
+// Top Ritz pair of T_m, block-wide, tuned for latency (round 3; replaces
+// block_check in the solver).  T_m's coefficients are loaded once into
+// registers (lane q holds alpha_q, beta^2_{q-1}, beta^2_q for q = lane and
+// lane + 64) and every serial chain takes them by v_readlane (no LDS latency
+// on a chain); the Gershgorin bounds [glo, ghi] are kept by the caller.
+//   1. the eigenvalue by multisection on Sturm counts over 256 points (64 per
+//      wave, one barrier per round; theta_lb / hint as in block_check);
+//   2. the eigenvector from the two three-term recurrences of (T - theta) f = 0
+//      in the division-free minor form: with pi_k = beta_0 ... beta_{k-1},
+//      g_k = f_k pi_k obeys g_{k+1} = (theta - alpha_k) g_k - beta^2_{k-1} g_{k-1}
+//      (one fma on the chain) and Q_k = pi_k^2 runs beside it -- forward from
+//      the top on wave 0, backward (h, R) from the bottom on wave 1 at the same
+//      time, both rescaled by powers of two every four steps;
+//   3. every lane forms, for its two indices, the twisted-factorisation
+//      gamma_k = (alpha_k - theta) + beta^2_{k-1} g_{k-1}/g_k + beta^2_k h_{k+1}/h_k
+//      (= d+_k + d-_k - (alpha_k - theta)), the twist r = argmin |gamma| (first
+//      index), and z_k = (g_k/g_r) sqrt(Q_r/Q_k) (k <= r), (h_k/h_r) sqrt(R_r/R_k)
+//      (k >= r): the twisted factorisation's vector, each half from its stable
+//      direction; normalised.
+// scr: >= kCheckScr doubles of LDS.  Every wave returns the same values; wave
+// 0 writes z[0, m).  The residual of the pair is beta_m |z_{m-1}|.
+constexpr int kCheckScr = 6 * MMAX + 32;
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a
+// workgroup-scope release fence, so it waits for the wave's outstanding
+// GLOBAL stores (vmcnt(0)) too -- in the Lanczos step that is the basis
+// vector just written to the per-workgroup scratch, an L2 round trip per
+// barrier for nothing the barrier protects.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ double rcp_nr(double b) {   // 1/b within ~1 ulp
+  const double r = __builtin_amdgcn_rcp(b);
+  return fma(fma(-b, r, 1.0), r, r);
+}
+
+__device__ __forceinline__ void fast_check(const double* T, int m, double theta_lb, double hint, double glo,
+                                           double ghi, double* z, double* scr, double* theta_out, double* zlast_out,
+                                           int* rounds_out, long long* ph = nullptr) {
+  m = __builtin_amdgcn_readfirstlane(m);
+  if (ph) ph[0] = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* gq = scr;                   // [MMAX] g | [MMAX] Q  (forward chain)
+  double* hr = scr + 2 * MMAX;        // [MMAX] h | [MMAX] R  (backward chain)
+  double* ex = scr + 4 * MMAX;        // [MMAX] exponents (fwd g, Q per block of 4) | [MMAX] (bwd)
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(scr + 6 * MMAX);   // [2][4]
+  const double a0 = T[0];
+  double lo = fmax(glo, fmax(theta_lb, a0));
+  double hi = ghi;
+  if (!(lo < hi)) lo = glo;
+  const bool hinted = hint >= 0.0 && theta_lb > -1e299;
+  const double hg = lo + 4.0 * hint + 4e-16 * fabs(lo);
+  if (ph) ph[1] = __builtin_amdgcn_s_memtime();
+  // Sturm count at x (det(T_k - x) signs; >= m <=> x above every eigenvalue).
+  // fp64 fma latency (~30 cycles for one wave) sets the pace: one fma per
+  // step on the chain, the (alpha, beta^2) pairs read from LDS (broadcast) a
+  // block of four ahead of their use.
+  const double2* T2 = reinterpret_cast<const double2*>(T);
+  auto count = [&](double x) -> int {
+    double p2 = 1.0, p1 = a0 - x;
+    unsigned cnt = static_cast<unsigned>(__builtin_bit_cast(unsigned long long, p1) >> 63);
+    auto step = [&](double2 t) __attribute__((always_inline)) {
+      const double pk = fma(t.x - x, p1, -(t.y * p2));
+      cnt += static_cast<unsigned>((__builtin_bit_cast(unsigned long long, pk) ^
+                                    __builtin_bit_cast(unsigned long long, p1)) >> 63);
+      p2 = p1;
+      p1 = pk;
+    };
+    double2 c0 = T2[1], c1 = T2[2];
+    int q = 1;
+    for (; q + 4 <= m; q += 4) {
+      const double2 c2 = T2[q + 2], c3 = T2[q + 3];
+      step(c0);
+      step(c1);
+      c0 = T2[q + 4];
+      c1 = T2[q + 5];
+      step(c2);
+      step(c3);
+      const int e = __builtin_amdgcn_frexp_exp(p1);
+      p1 = __builtin_amdgcn_ldexp(p1, -e);
+      p2 = __builtin_amdgcn_ldexp(p2, -e);
+    }
+    if (q < m) step(c0);
+    if (q + 1 < m) step(c1);
+    if (q + 2 < m) step(T2[q + 2]);
+    return static_cast<int>(cnt);
+  };
+  // Cold start (no previous Ritz value in this eigenproblem): Laguerre's
+  // method from the Gershgorin upper bound on det(x - T_m) = P(x) -- from above
+  // the largest root of a real-rooted polynomial it decreases monotonically to
+  // it, cubically once close (4-6 chains of m steps instead of ~7 multisection
+  // rounds); one uniform round of 256 points over +-64 ulps then brackets it to
+  // two ulps and verifies that it is the top eigenvalue (else the full
+  // multisection runs from the Gershgorin bracket).  Every wave computes the
+  // same (wave-uniform) iterates.
+  bool laguerre = false;
+  const double lo0 = lo, hi0 = hi;
+  if (!hinted && m > 2) {
+    double x = hi;
+    for (int itl = 0; itl < 16; ++itl) {
+      double p0 = 1.0, p1 = x - a0, d0 = 0.0, d1 = 1.0, e0 = 0.0, e1 = 0.0;
+      auto lstep = [&](double2 t) __attribute__((always_inline)) {
+        const double c = x - t.x;
+        const double pn = fma(c, p1, -(t.y * p0));
+        const double dn = fma(c, d1, p1 - t.y * d0);
+        const double en = fma(c, e1, 2.0 * d1 - t.y * e0);
+        p0 = p1; p1 = pn;
+        d0 = d1; d1 = dn;
+        e0 = e1; e1 = en;
+      };
+      double2 c0 = T2[1], c1 = T2[2];
+      int q = 1;
+      for (; q + 4 <= m; q += 4) {
+        const double2 c2 = T2[q + 2], c3 = T2[q + 3];
+        lstep(c0);
+        lstep(c1);
+        c0 = T2[q + 4];
+        c1 = T2[q + 5];
+        lstep(c2);
+        lstep(c3);
+        const int e = __builtin_amdgcn_frexp_exp(fmax(fabs(p1), fabs(d1)));
+        p0 = __builtin_amdgcn_ldexp(p0, -e); p1 = __builtin_amdgcn_ldexp(p1, -e);
+        d0 = __builtin_amdgcn_ldexp(d0, -e); d1 = __builtin_amdgcn_ldexp(d1, -e);
+        e0 = __builtin_amdgcn_ldexp(e0, -e); e1 = __builtin_amdgcn_ldexp(e1, -e);
+      }
+      if (q < m) lstep(c0);
+      if (q + 1 < m) lstep(c1);
+      if (q + 2 < m) lstep(T2[q + 2]);
+      if (!(p1 != 0.0)) break;   // x is an eigenvalue (or a NaN appeared): the bracket round decides
+      const double G = d1 / p1, H = G * G - e1 / p1;
+      const double nn = static_cast<double>(m);
+      const double den = G + sqrt(fmax((nn - 1.0) * (nn * H - G * G), 0.0));
+      const double xn = x - nn / den;
+      if (!(xn < x) || !(xn >= lo0)) break;
+      const bool fin = x - xn <= 4e-16 * fabs(x);
+      x = xn;
+      if (fin) break;
+    }
+    const double u = 64.0 * 2.2204460492503131e-16 * fabs(x);
+    if (x - u > lo0 && x + u < hi0) {
+      lo = x - u;
+      hi = x + u;
+      laguerre = true;
+    }
+  }
+  int round = 0;
+  for (; round < 24; ++round) {
+    const int kind = round == 0 ? (laguerre ? 3 : (hinted && hg < hi ? 1 : 2)) : 0;
+    const double rlo = lo, rhi = hi;
+    // kind 3: the Laguerre bracket, points at both ends included so that the
+    // round also verifies it
+    auto point = [&](int p) -> double {
+      if (kind == 1) return p < 255 ? rlo + (hg - rlo) * ((p + 1) * (1.0 / 255.0)) : rhi;
+      if (kind == 2) return rlo + (rhi - rlo) * __builtin_amdgcn_ldexp(1.0, p - 255);
+      if (kind == 3) return rlo + (rhi - rlo) * (p * (1.0 / 255.0));
+      return rlo + (rhi - rlo) * ((p + 1) * (1.0 / 257.0));
+    };
+    const unsigned long long ok = __builtin_amdgcn_ballot_w64(count(point(64 * wave + lane)) >= m);
+    unsigned long long* M = masks + 4 * (round & 1);
+    if (lane == 0) M[wave] = ok;
+    lds_barrier();
+    int first = 256;
+    for (int w = 3; w >= 0; --w)
+      if (M[w]) first = 64 * w + __builtin_ctzll(M[w]);
+    if (kind == 3 && (first == 0 || first == 256)) {
+      // the top eigenvalue is not inside the Laguerre bracket: full multisection
+      lo = lo0;
+      hi = hi0;
+      laguerre = false;
+      continue;
+    }
+    const double xf = first < 256 ? point(first) : rhi;
+    const double xb = first > 0 ? point(first - 1) : rlo;
+    const bool stalled = xb == lo && xf == hi;
+    lo = xb;
+    hi = xf;
+    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
+  }
+  const double lm = 0.5 * (lo + hi);
+  if (ph) ph[2] = __builtin_amdgcn_s_memtime();
+  // ---- the two eigenvector recurrences: wave 0 forward (row i produces
+  // index i + 1), wave 1 backward (row i produces index i - 1)
+  auto chain = [&](auto FWD) __attribute__((always_inline)) {
+    constexpr bool fwd = decltype(FWD)::value;
+    double* val = fwd ? gq : hr;
+    double* exb = ex + (fwd ? 0 : MMAX);
+    double g1 = 1.0, g0 = 0.0, qq = 1.0;
+    int eg = 0, eq = 0, k = 0;   // k = steps done = position of g1 along the chain
+    const int i0 = fwd ? 0 : m - 1;
+    // lane l keeps the values of indices l and l + 64 in registers (written
+    // to LDS once, after the chain)
+    double gv[2] = {0.0, 0.0}, qv[2] = {0.0, 0.0};
+    if ((i0 & 63) == lane) {
+      gv[i0 >> 6] = 1.0;
+      qv[i0 >> 6] = 1.0;
+    }
+    if (lane == 0) {
+      exb[0] = 0.0;
+      exb[1] = 0.0;
+    }
+    // Pair P_i = T2[i] = (alpha_i, beta^2_{i-1}).  fwd row i = k: behind =
+    // P_i.y, ahead = beta^2_i = P_{i+1}.y (the next step's pair); bwd row
+    // i = m-1-k: ahead = P_i.y, behind = beta^2_i = P_{i+1}.y (the previous
+    // step's pair).  Pairs are read two steps ahead of use; reads past the
+    // chain's end land in the record's padding / row 0 and are never used.
+    auto pr = [&](int kk) __attribute__((always_inline)) -> double2 {
+      int i = fwd ? kk : m - 1 - kk;
+      i = i < 0 ? 0 : i;
+      return T2[i];
+    };
+    double2 cur = pr(0), nx1 = pr(1), nx2 = pr(2);
+    double bbw = 0.0;   // bwd: behind coefficient (previous pair's .y); fwd: unused
+    auto step = [&](double2 c, double2 nxt) __attribute__((always_inline)) {
+      const double behind = fwd ? c.y : bbw;
+      const double ahead = fwd ? nxt.y : c.y;
+      const double gn = fma(lm - c.x, g1, -(behind * g0));
+      qq *= ahead;
+      if (!fwd) bbw = c.y;
+      g0 = g1;
+      g1 = gn;
+      const int idx = fwd ? k + 1 : m - 2 - k;
+      if ((k & 3) == 3) {
+        const int e = __builtin_amdgcn_frexp_exp(g1);
+        g1 = __builtin_amdgcn_ldexp(g1, -e);
+        g0 = __builtin_amdgcn_ldexp(g0, -e);
+        eg += e;
+        const int e2 = __builtin_amdgcn_frexp_exp(qq);
+        qq = __builtin_amdgcn_ldexp(qq, -e2);
+        eq += e2;
+        if (lane == 0) {
+          exb[2 * ((k + 1) >> 2)] = static_cast<double>(eg);
+          exb[2 * ((k + 1) >> 2) + 1] = static_cast<double>(eq);
+        }
+      }
+      const bool me = (idx & 63) == lane;
+      if (idx < 64) {
+        gv[0] = me ? g1 : gv[0];
+        qv[0] = me ? qq : qv[0];
+      } else {
+        gv[1] = me ? g1 : gv[1];
+        qv[1] = me ? qq : qv[1];
+      }
+      ++k;
+    };
+    const int steps = m - 1;
+    while (k + 2 <= steps) {
+      const double2 nx3 = pr(k + 3), nx4 = pr(k + 4);
+      step(cur, nx1);
+      step(nx1, nx2);
+      cur = nx2;
+      nx1 = nx3;
+      nx2 = nx4;
+    }
+    if (k < steps) step(cur, nx1);
+    val[lane] = gv[0];
+    val[MMAX + lane] = qv[0];
+    val[64 + lane] = gv[1];
+    val[MMAX + 64 + lane] = qv[1];
+  };
+  // the first step's "behind" coefficient multiplies g0 = 0
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  if (wu == 0) chain(std::integral_constant<bool, true>{});
+  else if (wu == 1) chain(std::integral_constant<bool, false>{});
+  lds_barrier();
+  if (ph) ph[3] = __builtin_amdgcn_s_memtime();
+  // exponents of a chain value by its position p along the chain: the rescale
+  // after step 4b+3 makes position 4b+4 the first of block b+1
+  auto pexp = [&](const double* exb, int p, int which) -> int {
+    return static_cast<int>(exb[2 * (p >> 2) + which]);
+  };
+  // ---- gamma, twist, z (every wave, identical)
+  double zv[2], gam = 1e308;
+  int tw = 0;
+#pragma unroll 1
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int k = lane + 64 * s2;
+    zv[s2] = 0.0;
+    if (k < m) {
+      double g = T[2 * k] - lm;
+      if (k > 0)
+        g += T[2 * k + 1] * __builtin_amdgcn_ldexp(gq[k - 1] * rcp_nr(gq[k]), pexp(ex, k - 1, 0) - pexp(ex, k, 0));
+      if (k + 1 < m)
+        g += T[2 * k + 3] * __builtin_amdgcn_ldexp(hr[k + 1] * rcp_nr(hr[k]),
+                                             pexp(ex + MMAX, m - 2 - k, 0) - pexp(ex + MMAX, m - 1 - k, 0));
+      const double ga = fabs(g);
+      if (ga < gam) {
+        gam = ga;
+        tw = k;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double og = __shfl_xor(gam, off);
+    const int ot = __shfl_xor(tw, off);
+    if (og < gam || (og == gam && ot < tw)) {
+      gam = og;
+      tw = ot;
+    }
+  }
+  tw = __builtin_amdgcn_readfirstlane(tw);
+  if (ph) ph[4] = __builtin_amdgcn_s_memtime();
+  const double igr = rcp_nr(gq[tw]), ihr = rcp_nr(hr[tw]);
+  const double qr = gq[MMAX + tw], rr = hr[MMAX + tw];
+  const int egr = pexp(ex, tw, 0), eqr = pexp(ex, tw, 1);
+  const int ehr = pexp(ex + MMAX, m - 1 - tw, 0), err = pexp(ex + MMAX, m - 1 - tw, 1);
+#pragma unroll 1
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int k = lane + 64 * s2;
+    if (k < m) {
+      if (k <= tw) {   // (g_k / g_r) sqrt(Q_r / Q_k)
+        int e2 = eqr - pexp(ex, k, 1);
+        double qratio = qr * rcp_nr(gq[MMAX + k]);
+        if (e2 & 1) { qratio *= 2.0; e2 -= 1; }
+        zv[s2] = __builtin_amdgcn_ldexp(gq[k] * igr * sqrt(qratio), pexp(ex, k, 0) - egr + e2 / 2);
+      } else {         // (h_k / h_r) sqrt(R_r / R_k)
+        int e2 = err - pexp(ex + MMAX, m - 1 - k, 1);
+        double rratio = rr * rcp_nr(hr[MMAX + k]);
+        if (e2 & 1) { rratio *= 2.0; e2 -= 1; }
+        zv[s2] = __builtin_amdgcn_ldexp(hr[k] * ihr * sqrt(rratio), pexp(ex + MMAX, m - 1 - k, 0) - ehr + e2 / 2);
+      }
+    }
+  }
+  const double inv = 1.0 / sqrt(wave_sum(zv[0] * zv[0] + zv[1] * zv[1]));
+  if (wave == 0) {
+    if (lane < m) z[lane] = zv[0] * inv;
+    if (lane + 64 < m) z[lane + 64] = zv[1] * inv;
+  }
+  lds_barrier();   // z is read by every wave (the Ritz vector) after the caller's next step or none
+  *zlast_out = rl_any(zv, m - 1) * inv;
+  *theta_out = lm;
+  *rounds_out = round + 1;
+  if (ph) ph[5] = __builtin_amdgcn_s_memtime();
+}
+
+// ---- lanczos_solve_kernel (round 3 layout) -------------------------------
+// Wave w holds rows 32w .. 32w + 31 of M: lane l has row 32w + (l & 31), the
+// column half 64 * (l >> 5) .. + 63 (64 doubles).  A 16-lane DPP row therefore
+// shares one column half, so the operator input reaches every lane through
+// v_fmac_f64_dpp row_newbcast (lane k of the DPP row holds x[64 half + 4k ..
+// + 3], two ds_read_b128 per lane per step instead of 32), and the two halves
+// of a row are added with one v_permlane32_swap (tools/ubench/lanczos_step.hip:
+// 1.68k vs 2.28k cycles per step alone, 1.23 vs 1.67 us per step at 3
+// workgroups per CU).
+constexpr int kTrw = 2 * MMAX + 32;   // T record: (alpha_q, beta^2_{q-1}) pairs, padded for the check's prefetch
+
 constexpr size_t kLanczosLds =
-    sizeof(double) * (XLEN + 2 * XLEN + 32 + TW + 2 * MMAX + (2 * MMAX + 16) + 64 + 4 * FNP + 240) +
+    sizeof(double) * (136 + 2 * 136 + 32 + kTrw + 2 * MMAX + kCheckScr + 64 + 4 * FNP + 240) +
     sizeof(int) * (3 * FNP + 16);
+static_assert(3 * kLanczosLds <= 163840, "three solver workgroups must fit one CU's LDS");
+
+__device__ __forceinline__ double swap_halves(double v) {   // the value of lane l ^ 32
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(b), static_cast<unsigned>(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(b >> 32), static_cast<unsigned>(b >> 32),
+                                                   false, false);
+  const bool up = (threadIdx.x & 63) >= 32;
+  const unsigned l = up ? lo[0] : lo[1], h = up ? hi[0] : hi[1];
+  return __builtin_bit_cast(double, (static_cast<unsigned long long>(h) << 32) | l);
+}
+
+#define SRA_FMAC_DPP(K, J)                                                                       \
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #K " row_mask:0xf bank_mask:0xf"        \
+               : "+v"(acc[J])                                                                     \
+               : "v"(xr[J]), "v"(g[4 * K + J]))
+#define SRA_FMAC_DPP4(K) SRA_FMAC_DPP(K, 0); SRA_FMAC_DPP(K, 1); SRA_FMAC_DPP(K, 2); SRA_FMAC_DPP(K, 3)
 
 template <int MODE, bool DBG>
 __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* xbuf = reinterpret_cast<double*>(smem);   // [XLEN] operator input
-  double* gbuf = xbuf + XLEN;                       // [XLEN] g = G w (forming M)
-  double* sbuf = gbuf + XLEN;                       // [XLEN] sqrt(w)
-  double* red = sbuf + XLEN;                        // [2][16] block reductions (parity slots)
-  double* trw = red + 32;                           // [TW] tridiagonal record (wave 0 runs the checks)
-  double* zbuf = trw + TW;                          // [2][MMAX] eigenvectors of T (current / best check)
-  double* cscr = zbuf + 2 * MMAX;                   // [2 MMAX + 16] check scratch (pivots, masks, result)
-  double* hbuf = cscr + 2 * MMAX + 16;              // [64] projection scalar
+  double* xbuf = reinterpret_cast<double*>(smem);   // [136] operator input
+  double* gbuf = xbuf + 136;                        // [136] g = G w (forming M)
+  double* sbuf = gbuf + 136;                        // [136] sqrt(w)
+  double* red = sbuf + 136;                         // [2][16] block reductions (parity slots)
+  double* trw = red + 32;                           // [kTrw] tridiagonal record
+  double* zbuf = trw + kTrw;                        // [2][MMAX] eigenvectors of T (current / best check)
+  double* cscr = zbuf + 2 * MMAX;                   // [kCheckScr] check scratch
+  double* hbuf = cscr + kCheckScr;                  // [64] projection scalar
   double* cvec = hbuf + 64;                         // [FNP] weights (projection / final scale)
   double* vscr = cvec + FNP;                        // [3][FNP] projection scratch
   double* clog = vscr + 3 * FNP;                    // [60][4] DBG: check log of the current iteration
@@ -1310,15 +1672,14 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int row = tid >> 1;
-  const int half = tid & 1;
+  const int row = 32 * wave + (lane & 31);
+  const int half = lane >> 5;
   const bool own = half == 0;
   const int n = A.n;
-  const int xi = row < 64 ? row : XOFF + row - 64;
   double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * MMAX * FNP;
 
   int rslot = 0;
-  auto reduce4 = [&](double v0, double v1, double (&o)[4], int nv) __attribute__((always_inline)) {
+  auto reduce2 = [&](double v0, double v1, double (&o)[4], int nv) __attribute__((always_inline)) {
     v0 = wave_sum(v0);
     if (nv > 1) v1 = wave_sum(v1);
     double* R = red + 16 * rslot;
@@ -1326,7 +1687,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       R[4 * wave + 0] = v0;
       if (nv > 1) R[4 * wave + 1] = v1;
     }
-    __syncthreads();
+    lds_barrier();
     o[0] = (R[0] + R[4]) + (R[8] + R[12]);
     if (nv > 1) o[1] = (R[1] + R[5]) + (R[9] + R[13]);
     rslot ^= 1;
@@ -1347,7 +1708,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       R[wave] = v;
       I[wave] = i;
     }
-    __syncthreads();
+    lds_barrier();
     double bv = R[0];
     int bi = I[0];
     for (int q = 1; q < 4; ++q)
@@ -1359,26 +1720,32 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
     *vbest = bv;
     return bi;
   };
+  if (tid < 16) trw[2 * MMAX + tid] = 0.0;   // prefetch padding of the T record
+  int* qslot = ibuf + 3 * FNP + 16 - 1;       // the chunk this workgroup took from the queue
 
-  for (int ch = blockIdx.x; ch < A.nb; ch += gridDim.x) {
+  // chunks come from a work queue (A.fb_count[4]): their cost varies with the
+  // Lanczos steps they need, a static split leaves a tail
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) *qslot = atomicAdd(A.fb_count + 4, 1);
+    __syncthreads();
+    const int ch = *qslot;
+    if (ch >= A.nb) break;
     const double2* Gr = reinterpret_cast<const double2*>(A.G + static_cast<size_t>(ch) * FNP * FNP + row * FNP +
                                                          64 * half);
     double g[64];   // G's row segment at the start of an iteration, then M's
-    // y = (this register matrix) x for x in xbuf; both lanes of the pair get the row value
+    // y = (this register matrix) x for x in xbuf; both lanes of the row get the value
     auto gmv = [&]() __attribute__((always_inline)) -> double {
-      const double2* xh = reinterpret_cast<const double2*>(xbuf + XOFF * half);
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-#pragma unroll
-      for (int c = 0; c < 32; c += 2) {
-        const double2 a = xh[c], b = xh[c + 1];
-        p0 = fma(g[2 * c], a.x, p0);
-        p1 = fma(g[2 * c + 1], a.y, p1);
-        p2 = fma(g[2 * c + 2], b.x, p2);
-        p3 = fma(g[2 * c + 3], b.y, p3);
-        if ((c & 6) == 6) asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)::"memory");
-      }
-      const double p = (p0 + p1) + (p2 + p3);
-      return p + dpp_f64<0xB1>(p);
+      const double2* xp = reinterpret_cast<const double2*>(xbuf + 64 * half + 4 * (lane & 15));
+      const double2 xa = xp[0], xb = xp[1];
+      double xr[4] = {xa.x, xa.y, xb.x, xb.y};
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      SRA_FMAC_DPP4(0); SRA_FMAC_DPP4(1); SRA_FMAC_DPP4(2); SRA_FMAC_DPP4(3);
+      SRA_FMAC_DPP4(4); SRA_FMAC_DPP4(5); SRA_FMAC_DPP4(6); SRA_FMAC_DPP4(7);
+      SRA_FMAC_DPP4(8); SRA_FMAC_DPP4(9); SRA_FMAC_DPP4(10); SRA_FMAC_DPP4(11);
+      SRA_FMAC_DPP4(12); SRA_FMAC_DPP4(13); SRA_FMAC_DPP4(14); SRA_FMAC_DPP4(15);
+      const double p = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      return p + swap_halves(p);
     };
 
     const bool dbg = DBG && ch == 0;
@@ -1393,9 +1760,9 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
     int m_hint = 24;
     double rate_hint = 0.0;
     bool fallback = false;
-    int done = 0;   // filter iterations completed (decision trace)
+    int clog_n = 0;
+    int done = 0;
     int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
-    int clog_n = 0;   // DBG: checks logged (per chunk, last 60 kept from the start)
 
     for (int it = 0; it < iters; ++it) {
       const long long t_it = dbg ? clock64() : 0;
@@ -1408,45 +1775,44 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         g[2 * c + 1] = v.y;
       }
       double o[4];
-      reduce4(own && ai ? ci : 0.0, own && ai ? 1.0 : 0.0, o, 2);
+      reduce2(own && ai ? ci : 0.0, own && ai ? 1.0 : 0.0, o, 2);
       const double csum = o[0];
       const int nact = static_cast<int>(o[1]);
       const double wi = ai ? ci / csum : 0.0;
       const double swi = sqrt(wi > 0.0 ? wi : 0.0);
       if (own) {
-        xbuf[xi] = wi;
-        sbuf[xi] = swi;
+        xbuf[row] = wi;
+        sbuf[row] = swi;
       }
-      __syncthreads();
+      lds_barrier();
       const double gwi = gmv();
-      if (own) gbuf[xi] = gwi;
-      reduce4(own ? wi * gwi : 0.0, 0.0, o, 1);
+      if (own) gbuf[row] = gwi;
+      reduce2(own ? wi * gwi : 0.0, 0.0, o, 1);
       const double sgw = o[0];
-      // ---- M = W^1/2 (G - g 1^T - 1 g^T + s 1 1^T) W^1/2 in place (the Gram of
-      // sqrt(w_i) (x_i - mu): its nonzero spectrum is the weighted covariance's)
+      // ---- M = W^1/2 (G - g 1^T - 1 g^T + s 1 1^T) W^1/2 in place
       {
-        const double2* gh = reinterpret_cast<const double2*>(gbuf + XOFF * half);
-        const double2* sh = reinterpret_cast<const double2*>(sbuf + XOFF * half);
+        const double2* gh = reinterpret_cast<const double2*>(gbuf + 64 * half);
+        const double2* sh = reinterpret_cast<const double2*>(sbuf + 64 * half);
         const double ri = sgw - gwi;
 #pragma unroll
         for (int c = 0; c < 32; ++c) {
           const double2 gj = gh[c], sj = sh[c];
           g[2 * c] = swi * ((g[2 * c] + ri - gj.x) * sj.x);
           g[2 * c + 1] = swi * ((g[2 * c + 1] + ri - gj.y) * sj.y);
+          // at most four (g, sqrt w) pieces in flight: the compiler would
+          // otherwise hoist all 64 LDS reads (128 VGPRs beside the 128 of M)
+          if ((c & 3) == 3) asm volatile("" : "+v"(g[2 * c]), "+v"(g[2 * c + 1])::"memory");
         }
       }
 
-      // ---- top eigenpair of M by plain Lanczos.  The computed residual of the
-      // top Ritz pair falls to a floor of ~1e-16 lambda and grows again once a
-      // ghost copy forms, so the best check so far is kept and accepted when
-      // the residual stalls at the floor; near convergence every step is
-      // checked.  A ghost before an acceptable residual restarts the
-      // eigenproblem once with dense checks.
+      // ---- top eigenpair of M by plain Lanczos (see the round-2 notes above
+      // lanczos_solve_kernel's declaration history in DESIGN.md k6): checks by
+      // fast_check, best residual kept, a ghost retries once with dense checks
       double lam = 0.0, resid = 0.0, ui = 0.0;
       int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
       bool converged = false;
       double tscale = 0.0;
-      long long tcheck = 0, tmult = 0, tvec = 0;   // diagnostics: cycles in checks
+      long long tcheck = 0;
       int trounds = 0;
       for (int attempt = 0; attempt < 2 && !converged; ++attempt) {
         double rt;
@@ -1454,15 +1820,15 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
           const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
           rt = swi > 0.0 ? swi * hh : 0.0;
         }
-        if (own) xbuf[xi] = rt;
-        reduce4(own ? rt * rt : 0.0, 0.0, o, 1);
+        if (own) xbuf[row] = rt;
+        reduce2(own ? rt * rt : 0.0, 0.0, o, 1);
         double nrm2 = o[0];
         double qprev = 0.0, theta_lb = -1e300, hint = -1.0;
         double res_best = 1e300, lam_best = 0.0;
         int m_best = 0;
         tscale = 0.0;
-        // the retry samples the residual every step from the check before the
-        // first attempt's best one (the sequence is the same: only the sampling differs)
+        // incremental Gershgorin bounds of T: rows 0 .. j-2 final, plus row j-1
+        double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
         const int adv_max = attempt == 0 ? kMaxAdvance : 1;
         int next_check = attempt == 0 ? (m_hint - 8 > 4 ? m_hint - 8 : 4) : (m_retry > 4 ? m_retry : 4);
         int m_a = -1, m_last = 4, m_pre = 4;
@@ -1477,12 +1843,11 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
             if (breakdown || j == MMAX || j >= next_check) {
               const int m = j;
               ++nchecks;
-              // top Ritz pair of T_m, block-wide (the record was written by
-              // thread 0: the barriers since order it for the other waves)
               const long long tc0 = dbg ? clock64() : 0;
               double lm, zl;
               int rounds = 0;
-              block_check(trw, m, theta_lb, hint, tscale, zbuf + zcur * MMAX, cscr, &lm, &zl, &rounds);
+              const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
+              fast_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, cscr, &lm, &zl, &rounds);
               if (dbg) {
                 tcheck += clock64() - tc0;
                 trounds += rounds;
@@ -1515,13 +1880,9 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
                 zbest = zcur;
                 zcur ^= 1;
               }
-              // past the floor: the residual grows again after it was small (a
-              // ghost copy is forming; a bump during slow convergence is not one)
               ghost = res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
               const bool out_of_steps = j == MMAX;
               if (ghost || out_of_steps) {
-                // the first attempt sampled the residual every few steps: the
-                // retry samples every step from the check before the best one
                 if (tid == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
                 m_retry = m_pre;
                 break;
@@ -1530,7 +1891,6 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
               double rate = rate_hint;
               if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
               if (rate < 0.0 && res > 0.0) {
-                // straight to the predicted step of the floor (kAccept)
                 const double need = log(kAccept * fabs(lm) / res) / rate;
                 adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
               }
@@ -1539,6 +1899,10 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
               m_last = m;
               next_check = m + adv;
             }
+            // row j-1 is final now that beta_{j-1} is known
+            gfin_hi = fmax(gfin_hi, a_last + b_prev + bet);
+            gfin_lo = fmin(gfin_lo, a_last - b_prev - bet);
+            b_prev = bet;
           }
           // y = M r~ (r~ = beta q_j in xbuf), alpha_j = q_j . M q_j
           const double y = gmv();
@@ -1546,25 +1910,27 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
           const double q = rt * ib;
           if (own) Vb[j * FNP + row] = q;
           const double mq = y * ib;
-          reduce4(own ? q * mq : 0.0, 0.0, o, 1);
+          reduce2(own ? q * mq : 0.0, 0.0, o, 1);
           const double aj = o[0];
           const double r = mq - aj * q - (j > 0 ? bet * qprev : 0.0);
           if (tid == 0) trw[2 * j] = aj;
+          a_last = aj;
           tscale = fmax(tscale, fabs(aj));
           qprev = q;
           rt = r;
-          if (own) xbuf[xi] = r;
-          reduce4(own ? r * r : 0.0, 0.0, o, 1);
+          if (own) xbuf[row] = r;
+          reduce2(own ? r * r : 0.0, 0.0, o, 1);
           nrm2 = o[0];
         }
-        if (!ghost) break;   // out of steps without an acceptable residual: no retry
+        if (!ghost) break;
       }
       if (!converged) {
         fallback = true;
         break;
       }
-      // ---- Ritz vector u = V z of the accepted check (the basis rows this lane
-      // pair's even lane wrote, ordered by the barriers since)
+      // ---- Ritz vector u = V z of the accepted check (the basis rows this
+      // wave's even lanes stored; let the stores land before reading them back)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       {
         const double* zb = zbuf + zbest * MMAX;
         double u0 = 0.0, u1 = 0.0;
@@ -1591,16 +1957,16 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
           rec[FNP + 7] = 0;
           rec[FNP + 8] = static_cast<double>(clock64() - t_it);
           rec[FNP + 9] = static_cast<double>(tcheck);
-          rec[FNP + 10] = static_cast<double>(tmult);
-          rec[FNP + 11] = static_cast<double>(tvec);
+          rec[FNP + 10] = 0;
+          rec[FNP + 11] = 0;
           rec[FNP + 12] = trounds;
         }
       }
       // ---- early exit (robust_estimator.py:163-164 / :71-72)
       if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
-      // ---- tau_i = ((x_i - mu).v)^2 = (C W^1/2 u)_i^2 / lambda = ((M u)_i / sqrt(w_i))^2 / lambda
-      if (own) xbuf[xi] = ui;
-      __syncthreads();
+      // ---- tau_i = ((M u)_i / sqrt(w_i))^2 / lambda
+      if (own) xbuf[row] = ui;
+      lds_barrier();
       const double mu_i = gmv();
       const double cu = swi > 0.0 ? mu_i / swi : 0.0;
       const double ti = cu * cu / lam;
@@ -1608,7 +1974,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         double tmax = 0.0;
         const int p = argmax_first(own && ai ? ti : -__builtin_inf(), row, &tmax);
         const double cn = (ai && row != p) ? ci * (1.0 - ti / tmax) : 0.0;
-        reduce4(own ? fabs(cn) : 0.0, 0.0, o, 1);
+        reduce2(own ? fabs(cn) : 0.0, 0.0, o, 1);
         ci = cn / o[0];
         if (row == p) ai = false;
         if (tr != nullptr && tid == 0) tr[1 + it] = p;
@@ -1624,15 +1990,15 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         if (tr != nullptr && tid == 0) tr[1 + it] = capped;
       }
       done = it + 1;
-      __syncthreads();   // every wave's gmv reads of xbuf before the next iteration writes it
+      lds_barrier();   // every wave's gmv reads of xbuf before the next iteration writes it
     }
 
-    __syncthreads();
+    lds_barrier();
     if (fallback) {
       if (tid == 0) {
         const int k = atomicAdd(A.fb_count, 1);
         A.fb_list[k] = ch;
-        if (DBG && k == 0 && A.dbg != nullptr) {   // check log of the first listed chunk (records 250 on)
+        if (DBG && k == 0 && A.dbg != nullptr) {
           double* lg = A.dbg + FNP * FNP + 250 * kDbgRec;
           for (int e = 0; e < 4 * (clog_n < 60 ? clog_n : 60); ++e) lg[e] = clog[e];
         }
@@ -1647,7 +2013,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       if (tr != nullptr) tr[1 + FNP + row] = ai ? 1 : 0;
     }
     if (tr != nullptr && tid == 0) tr[0] = done;
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
       int q2 = 0;
       double* kept = vscr;
@@ -1655,7 +2021,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         if (ibuf[2 * FNP + i]) kept[q2++] = cvec[i];
       A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -1691,7 +2057,7 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
 // ============================================================================
 // per chunk of a batch: G, weights, scalars, kept flags, fallback list slot
 constexpr size_t kChunkWsBytes = sizeof(double) * (FNP * FNP + FNP + kMisc) + sizeof(int) * (FNP + 1);
-constexpr int kLanczosGrid = 1024;   // workgroups of lanczos_solve_kernel (each owns a basis slot)
+constexpr int kLanczosGrid = 512;    // workgroups of lanczos_solve_kernel: 2 per CU, each owns a basis slot
 
 size_t filter_workspace_bytes(int64_t d, int itv) {
   const int64_t nchunks = cdiv(d, itv);
@@ -1718,7 +2084,8 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   double* Vws = mws + static_cast<size_t>(bmax) * kMisc;
   int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(lgrid_max) * MMAX * FNP);
   int* fbl = aws + static_cast<size_t>(bmax) * FNP;
-  int* fbc = fbl + bmax;   // [0] listed chunks, [1] ghost after the retry, [2] out of steps, [3] retries
+  int* fbc = fbl + bmax;   // [0] listed chunks, [1] ghost after the retry, [2] out of steps, [3] retries,
+                           // [4] lanczos_solve_kernel's chunk queue
   const void* solve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<0, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<0, false>))
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
@@ -1743,7 +2110,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     }
     SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
                  trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr};
-    SRA_HIP(hipMemsetAsync(fbc, 0, 4 * sizeof(int), s));
+    SRA_HIP(hipMemsetAsync(fbc, 0, 8 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
     if (mode == 1) {
       // ex_noregret damps the top direction gently, so its top two eigenvalues

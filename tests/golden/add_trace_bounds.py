@@ -12,9 +12,11 @@ none of which is the reference's own sequential outer-product sum (:158):
 the k x k covariance GEMM in two client orders ("gemm", "reverse") and the
 n x n client-space form ("dual"):
 
-  agree[chunk] = the number of leading iterations on which all three make the
-                 reference's decision (= the iteration count when they agree
-                 throughout);
+  agree[chunk] = the number of leading iterations on which all three, and the
+                 client-space form under four 1e-13 relative nudges of the
+                 weights (oracle.trace_pair: a decision such a nudge flips is
+                 a near-tie that rounding decides), make the reference's
+                 decision (= the iteration count when they agree throughout);
   bound[chunk] = 3 * max over the three of |oracle - ref| / max|ref|.
 
 The engine must reproduce the reference's decisions on the agreed prefix and
@@ -31,7 +33,12 @@ import os
 import sys
 import warnings
 
-import numpy as np
+# one BLAS thread: a threaded LAPACK/BLAS reduction order differs run to run,
+# and these chaotic iterations turn that into different bounds
+for _v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS"):
+    os.environ[_v] = "1"
+
+import numpy as np  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
@@ -46,6 +53,7 @@ def main():
         mode = 1 if func == "ex_noregret" else 0
         args = (list(x), p["eps"], p["sigma"], p["expansion"], p["itv"])
         outs, traces = [], []
+        n = z["trace"].shape[1] // 2
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             for order in (("gemm", "dual") if mode else ("gemm", "reverse", "dual")):
@@ -56,7 +64,28 @@ def main():
                     outs.append(orc.mom_filterL2(*args, p["delta"], order=order, trace=tr))
                 else:
                     outs.append(orc.filterL2(*args, order=order, trace=tr))
-                traces.append(orc.trace_array(tr, mode, z["trace"].shape[1] // 2))
+                traces.append(orc.trace_array(tr, mode, n))
+            # rounding-sized nudges of the weights (oracle.trace_pair): a
+            # decision they flip is a near-tie, outside the agreed prefix
+            rows = x.reshape(x.shape[0], -1)
+            if func == "mom_filterL2":
+                num, size = orc.bucket_count(rows.shape[0], p["eps"], p["delta"])
+                rows = np.asarray(orc.bucket_means(list(rows), size, num))
+            extra = []
+            for lo in range(0, rows.shape[1], p["itv"]):
+                a, _, _ = orc.trace_pair((rows[:, lo:lo + p["itv"]], mode, p["eps"], p["sigma"], p["expansion"]))
+                extra.append(a[:1 + n])
+            traces.append(np.array(extra))
+            for seed in range(orc.PERTURB_TRIALS):
+                tr = []
+                for lo in range(0, rows.shape[1], p["itv"]):
+                    ch = rows[:, lo:lo + p["itv"]]
+                    pt = (seed, orc.PERTURB_SCALE)
+                    if mode:
+                        orc.ex_noregret_(ch, p["eps"], p["sigma"], p["expansion"], trace=tr, order="dual", perturb=pt)
+                    else:
+                        orc.filterL2_(ch, p["eps"], p["sigma"], p["expansion"], order="dual", trace=tr, perturb=pt)
+                traces.append(orc.trace_array(tr, mode, n))
         bound, agree = [], []
         for i, lo in enumerate(range(0, ref.shape[0], p["itv"])):
             sl = slice(lo, lo + p["itv"])

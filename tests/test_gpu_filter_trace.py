@@ -16,8 +16,10 @@ pinned here through sra_filter_trace_f32:
   is agreed, and lands within the chunk's bound (3x the farthest oracle
   evaluation from the reference);
 * full size (C4 N=128 x d=1e7, C5 per GPU N=512 x d=1.25e7): 24 chunks
-  (first, last, random) against the oracle's client-space evaluation in two
-  client orders ("dual", "dual_reverse"), on the prefix where those two agree.
+  (first, last, random) against the oracle's client-space evaluation
+  (oracle.robust_np.trace_pair), on the prefix where it makes the same
+  decisions in two client orders and under four 1e-13 relative nudges of the
+  weights (a decision such a nudge flips is a near-tie that rounding decides).
 """
 from __future__ import annotations
 
@@ -102,15 +104,23 @@ def _fullsize(X, mode, nsample=24, seed=0):
     with mp.get_context("spawn").Pool(min(8, len(args))) as pool:
         refs = pool.map(orc.trace_pair, args)
     agreed = 0
-    for c, (a, b) in zip(chunks, refs):
-        diff = np.nonzero(a[1:1 + a[0]] != b[1:1 + a[0]])[0]
-        agree = int(diff[0]) if diff.size else (int(a[0]) if a[0] == b[0] else int(min(a[0], b[0])))
+    for c, (a, agree, margin) in zip(chunks, refs):
         agreed += agree == a[0]
-        _check_prefix(tr[c], a, agree, n, "chunk %d" % c)
+        got = tr[c]
+        diff = np.nonzero(got[1:1 + a[0]] != a[1:1 + a[0]])[0]
+        print("chunk %5d: agreed prefix %2d of %2d, first device difference at %s (oracle margin there %s)" % (
+            c, agree, a[0], diff[0] if diff.size else "-",
+            "%.1e" % margin[diff[0]] if diff.size and diff[0] < len(margin) else "-"))
+        _check_prefix(got, a, agree, n, "chunk %d" % c)
         if mode == 1:   # the Krum pre-filter's kept set
-            np.testing.assert_array_equal(tr[c, 1 + n:], a[1 + n:], err_msg="chunk %d: kept set" % c)
+            np.testing.assert_array_equal(got[1 + n:], a[1 + n:], err_msg="chunk %d: kept set" % c)
     assert np.isfinite(out.cpu().numpy()).all()
-    assert agreed >= len(chunks) // 2
+    # the agreed prefixes must cover most of the run (the early iterations
+    # remove the far-out Byzantine clients; the near ties come late)
+    total = sum(int(a[0]) for a, _, _ in refs)
+    covered = sum(ag for _, ag, _ in refs)
+    print("decisions compared: %d of %d (%d chunks fully agreed)" % (covered, total, agreed))
+    assert covered >= 0.6 * total
     return agreed, len(chunks)
 
 

@@ -92,7 +92,8 @@ def test_filter_chunks_independent_and_full_size_smoke():
     out = engine.filter_l2(Y, 0.2, 1e-5, 20, 1000).cpu().numpy()
     assert np.isfinite(out).all()
     # benign-only data: the hardest case for the eigensolver (clustered spectrum)
-    _chunk_check(Y, out, [999], lambda xs, o: orc.filterL2(xs, 0.2, 1e-5, 20, 1000, order=o))
+    _chunk_check(Y, out, [999], lambda xs, o, pt, tr: orc.filterL2(xs, 0.2, 1e-5, 20, 1000, order=o, perturb=pt,
+                                                                     trace=tr), 0)
 
 
 def test_filter_internals_chunk0():
@@ -134,49 +135,87 @@ def _device_rows(n, d, byz, seed):
     return X
 
 
-def _chunk_check(X, got, chunks, oracle_fn, orders=("gemm", "reverse", "dual"), floor=0.0):
+def _chunk_check(X, got, chunks, oracle_fn, mode, orders=("gemm", "reverse", "dual", "nudge"), floor=0.0,
+                 gtrace=None):
     """Device result on whole chunks vs the oracle's first evaluation order.
+
     filterL2's 50 iterations carry rounding to 1e-6 .. 1e-2 of max|out|
-    (DESIGN.md §4), so the bound is 3x the farthest of the oracle's other
-    independent fp64 evaluations from the first one (the rule of
+     even with identical decisions, and late near-tie decisions
+    themselves flip under rounding (tests/test_gpu_filter_trace.py pins the
+    decisions).  So the output bound is measured per chunk: 3x the farthest,
+    from the checker (the first order), of the oracle's other independent fp64
+    evaluations that make the checker's decisions -- "reverse", "dual" and the
+    four 1e-13 relative weight nudges of oracle.trace_pair ("nudge") --
+    relative to the chunk's max|out| (the rule of
     tests/golden/add_trace_bounds.py, with the oracle standing in for the
-    reference at full size), relative to the chunk's max|out|; ``floor`` is a
-    relative lower bound (ex_noregret's fp32 step, add_trace_bounds.py)."""
+    reference at full size).  A chunk whose device trace (``gtrace``) differs
+    from the checker's late in the run is reported and not compared; ``floor``
+    is a relative lower bound (ex_noregret's fp32 step, add_trace_bounds.py)."""
+    compared = 0
     for c in chunks:
         lo, hi = c * 1000, min((c + 1) * 1000, X.shape[1])
         xs = list(X[:, lo:hi].cpu().numpy())
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
-            outs = [oracle_fn(xs, o) for o in orders]
-        m = np.abs(outs[0]).max()
-        spread = max([np.abs(o - outs[0]).max() for o in outs[1:]] + [0.0]) / m
+            runs = []
+            for o in orders:
+                for pt in ([(s, orc.PERTURB_SCALE) for s in range(orc.PERTURB_TRIALS)] if o == "nudge" else [None]):
+                    tr = []
+                    out = oracle_fn(xs, "dual" if o == "nudge" else o, pt, tr)
+                    runs.append((out, orc.trace_array(tr, mode, X.shape[0])[0]))
+        out0, tr0 = runs[0]
+        m = np.abs(out0).max()
+        same = [o for o, t in runs[1:] if (t == tr0).all()]
+        err = np.abs(got[lo:hi] - out0).max() / m
+        if gtrace is not None and not (gtrace[c, :1 + X.shape[0]] == tr0).all():
+            print("chunk %d: device decisions differ from the checker's late in the run; error %.2e of max "
+                  "not compared" % (c, err))
+            continue
+        if not same and floor == 0.0:
+            print("chunk %d: no other oracle evaluation makes the checker's decisions; not compared" % c)
+            continue
+        spread = max([np.abs(o - out0).max() for o in same] + [0.0]) / m
         bound = max(3.0 * spread, floor)
-        err = np.abs(got[lo:hi] - outs[0]).max() / m
-        print("chunk %d: error %.2e of max, bound %.2e" % (c, err, bound))
+        print("chunk %d: error %.2e of max, bound %.2e (%d of %d oracle runs share the decisions)" % (
+            c, err, bound, len(same), len(runs) - 1))
         assert err <= bound, "chunk %d: %.3e of max > bound %.3e" % (c, err, bound)
+        compared += 1
+    assert compared >= 1
 
 
 def test_c4_filterl2_fullsize_chunks():
     """C4: filterl2, N=128 x d=1e7, against the oracle on 3 chunks."""
     X = _device_rows(128, 10_000_000, 20, seed=41)
-    got = engine.filter_l2(X, **SIM).cpu().numpy()
+    got, gtr = engine.filter_trace(X, 0, **SIM)
+    got = got.cpu().numpy()
     assert np.isfinite(got).all()
-    _chunk_check(X, got, [0, 4321, 9999], lambda xs, o: orc.filterL2(xs, order=o, **SIM))
+    np.testing.assert_array_equal(got, engine.filter_l2(X, **SIM).cpu().numpy())
+    _chunk_check(X, got, [0, 4321, 9999],
+                 lambda xs, o, pt, tr: orc.filterL2(xs, order=o, perturb=pt, trace=tr, **SIM), 0, gtrace=gtr)
 
 
 def test_c4_ex_noregret_fullsize_chunks():
     """C4: ex_noregret, N=128 x d=1e7 (eps = malnum/nworker = 0.2), against the oracle on 3 chunks."""
     X = _device_rows(128, 10_000_000, 20, seed=42)
-    got = engine.ex_noregret(X, **SIM).cpu().numpy()
+    got, gtr = engine.filter_trace(X, 1, **SIM)
+    got = got.cpu().numpy()
     assert np.isfinite(got).all()
-    _chunk_check(X, got, [0, 5678, 9999], lambda xs, o: orc.ex_noregret(xs, order=o, **SIM), ("dual",), 2e-5)
+    _chunk_check(X, got, [0, 5678, 9999],
+                 lambda xs, o, pt, tr: orc.ex_noregret(xs, order=o, trace=tr, **SIM), 1, ("gemm",), 2e-5, gtr)
 
 
 def test_c5_mom_filterl2_per_gpu_shard_chunks():
     """C5 per GPU: mom_filterl2, N=512 x d=1.25e7, delta = e^-26 (128 buckets of 4),
-    against the oracle on 2 chunks."""
+    against the oracle on 2 chunks of the (bit-exact, tests/test_gpu_krum.py)
+    device bucket means."""
     delta = float(np.exp(-26))
     X = _device_rows(512, 12_500_000, 100, seed=43)
     got = engine.mom_filter_l2(X, delta=delta, **SIM).cpu().numpy()
+    num, size = engine.mom_bucket_count(512, SIM["eps"], delta)
+    B = engine.bucket_means(X, size, num)
+    del X
+    got2, gtr = engine.filter_trace(B, 0, **SIM)
+    np.testing.assert_array_equal(got, got2.cpu().numpy())
     assert np.isfinite(got).all()
-    _chunk_check(X, got, [0, 12499], lambda xs, o: orc.mom_filterL2(xs, delta=delta, order=o, **SIM))
+    _chunk_check(B, got, [0, 12499],
+                 lambda xs, o, pt, tr: orc.filterL2(xs, order=o, perturb=pt, trace=tr, **SIM), 0, gtrace=gtr)
