@@ -221,6 +221,21 @@ def solver_flops(agg, X, itv=1000):
     return per_chunk * nchunks, iters
 
 
+def filter_into(agg):
+    """(X_cols, out_view) form of a spectral filter for the pipelined path: the
+    block's result is written straight into its slot of the all-gather buffer."""
+    ffn = {"filterl2": engine.filter_l2, "ex_noregret": engine.ex_noregret,
+           "mom_filterl2": engine.mom_filter_l2, "mom_ex_noregret": engine.mom_ex_noregret}[agg]
+    kw = dict(FILTER_ARGS, check=False)
+    if agg.startswith("mom_"):
+        kw["delta"] = MOM_DELTA
+
+    def into(Xc, o):
+        ffn(Xc, out=o, **kw)
+    into.out_dtype = torch.float64
+    return into
+
+
 def filter_block(d, chunks, itv):
     """Block width for the pipelined filter path: d split into the largest
     number <= chunks of equal blocks that are whole itv-chunks (the filters
@@ -349,13 +364,7 @@ def main():
         block = filter_block(d, a.chunks, FILTER_ARGS["itv"])
         if block:
             pipelined = True
-            into = lambda Xc, o: o.copy_(fn_into(Xc))   # noqa: E731
-            ffn = {"filterl2": engine.filter_l2, "ex_noregret": engine.ex_noregret,
-                   "mom_filterl2": engine.mom_filter_l2, "mom_ex_noregret": engine.mom_ex_noregret}[a.agg]
-            if a.agg.startswith("mom_"):
-                fn_into = lambda Xc: ffn(Xc, delta=MOM_DELTA, check=False, **FILTER_ARGS)   # noqa: E731
-            else:
-                fn_into = lambda Xc: ffn(Xc, check=False, **FILTER_ARGS)   # noqa: E731
+            into = filter_into(a.agg)
     comm = torch.cuda.Stream(device=device) if pipelined else None
 
     def step(ev=None):

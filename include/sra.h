@@ -82,8 +82,12 @@ int sra_gram_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
 
 /* G (n x n, fp64, row-major, symmetric) = centred Gram of the clients:
  * G_ij = sum_k (X[i,k] - mu_k)(X[j,k] - mu_k) with mu a per-coordinate shift,
- * so ||x_i - x_j||^2 = G_ii + G_jj - 2 G_ij.  fp32 MFMA, fp64 reduction.
- * 1 <= n <= 256.  Feeds krum_ (src/robust_estimator.py:234-244). */
+ * so ||x_i - x_j||^2 = G_ii + G_jj - 2 G_ij.  bf16 MFMA on an exact three-way
+ * split of every centred fp32 value (six products per term: fp32-product
+ * accuracy), fp32 partials per k-group, fp64 reduction.
+ * 1 <= n <= 512 (n > 256: one launch per pair of 128-client blocks, all
+ * centred by the fp32 mean over the n clients).  Feeds krum_
+ * (src/robust_estimator.py:234-244). */
 int sra_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes,
                  void* stream);
 
@@ -134,7 +138,9 @@ int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32_t mode, si
  * whose nearest client is removed), then the per-coordinate Bulyan median
  * with numpy's fp64 pairwise tie-break and the mean of the beta = theta - 2f
  * nearest values.  out: d float64 values.  selected (optional, theta int32):
- * the chosen clients in krum mode.  theta <= 0 -> SRA_ERR_THETA. */
+ * the chosen clients in krum mode.  theta <= 0 -> SRA_ERR_THETA.
+ * 1 <= n <= 512 (more than 128 remaining clients: LDS k-select + distance
+ * passes per round; theta > 128: an LDS-sorted per-coordinate stage). */
 int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
                    int32_t* selected, void* ws, size_t ws_bytes, void* stream);
 
@@ -145,7 +151,9 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
  * coordinate-wise median (mode 1) or trimmed mean (mode 2; dba != 0: the DBA
  * harness's lower median, src/DBA/helper.py:1025) of the listed rows; dist[r]
  * (nr doubles) = squared L2 distance of listed row r to agg over this block's
- * columns.  Column shards' dist vectors sum to the full distance.  N <= 128;
+ * columns.  Column shards' dist vectors sum to the full distance (up to fp64
+ * rounding: the per-tile partials are associated differently).  N <= 512
+ * (rounds with more than 128 listed rows take an LDS k-select + distance pass);
  * workspace from sra_bulyan_round_workspace_bytes. */
 int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes);
 int sra_bulyan_round_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const int32_t* rows, int32_t nr,
@@ -161,7 +169,7 @@ int sra_bulyan_pick(const double* dist, const int32_t* rows, int32_t nr, int32_t
  * i-th selected vector in selection order, row stride lds): out[j] (float64)
  * as sra_bulyan_f32's final stage computes it for robust_estimator.py:324-330
  * (bulyan_one_coordinate over np_grads[:, j], beta = theta - 2f, Python slice
- * semantics for beta < 0).  1 <= theta <= 128; workspace from
+ * semantics for beta < 0).  1 <= theta <= 512; workspace from
  * sra_bulyan_stage_workspace_bytes (8 d bytes plus a few hundred). */
 int sra_bulyan_stage_workspace_bytes(int64_t theta, int64_t d, size_t* bytes);
 int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, int64_t lds, int32_t beta, double* out,
@@ -184,14 +192,16 @@ int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t d, int64_t
 
 /* Workspace for sra_filter_f32 / sra_filter_debug_f32, in bytes: the n x n
  * (padded 128 x 128) fp64 Gram, weights and flags of up to 8192 chunks at a
- * time (longer layers are processed in batches of 8192 chunks). */
+ * time (longer layers are processed in batches of 8192 chunks; 256 chunks
+ * of n x n for n > 128). */
 int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes);
 
 /* mode 0: robust_estimator.filterL2 (src/robust_estimator.py:144-208);
  * mode 1: robust_estimator.ex_noregret (src/robust_estimator.py:42-133).
  * The layer (n x d) is cut into itv-wide chunks (last one partial); each chunk
  * is filtered in client space from its centred fp64-MFMA Gram (top eigenpair
- * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 128.
+ * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 512 (n > 128: the
+ * Gram in global memory, a 1024-thread re-orthogonalising solver per chunk).
  * status: device int32, zeroed by the caller; set to 2 when an ex_noregret
  * projection has no feasible candidate (the reference then fails with
  * TypeError).  ex_noregret with ceil(eps*n) = 0 or fewer than 2 clients left
@@ -201,14 +211,15 @@ int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mo
                    void* stream);
 
 /* As sra_filter_f32, and records every chunk's discrete decisions into trace
- * (device int32, nchunks x SRA_FILTER_TRACE_STRIDE; replaces nothing in the
+ * (device int32, nchunks rows of 1 + 2 * H int32, H = max(n, 128), i.e.
+ * SRA_FILTER_TRACE_STRIDE for n <= 128; replaces nothing in the
  * reference -- it exposes what robust_estimator.py:163-174 / :49-51, :71-99
  * decide, so tests can pin them):
  *   [0]            iterations completed (< T when the early exit fired)
  *   [1 + it]       filterL2: the client removed at iteration it (argmax tau,
  *                  first index, original numbering); ex_noregret: how many
  *                  weights the kept KL-projection candidate caps
- *   [1 + 128 + i]  1 if client i is active at the end (filterL2: not removed;
+ *   [1 + H + i]    1 if client i is active at the end (filterL2: not removed;
  *                  ex_noregret: kept by the Krum pre-filter), else 0
  * Unused decision slots are left untouched. */
 #define SRA_FILTER_TRACE_STRIDE (1 + 2 * 128)

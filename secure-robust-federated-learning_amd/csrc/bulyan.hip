@@ -37,7 +37,6 @@ int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds
 size_t krum_workspace_bytes(int n, int64_t d);
 
 enum BulyanMode { kBulyanKrum = 0, kBulyanMedian = 1, kBulyanTrimmed = 2 };
-constexpr int kMaxClientsBulyan = 256;
 
 // ---------------------------------------------------------------------------
 // k-select over a device row list (median / trimmed mean of the remaining set)
@@ -272,7 +271,6 @@ static int64_t round_blocks(int64_t d) { return cdiv(cdiv(d, 256), round_tiles_p
 static size_t round_partial_bytes(int n, int64_t d) {
   return sizeof(float) * static_cast<size_t>(n) * static_cast<size_t>(round_blocks(d));
 }
-constexpr size_t kRoundPartialMaxBytes = sizeof(float) * 128 * kRoundMaxBlocks;
 
 // argmin (first strict minimum, NaN never chosen) of the listed rows'
 // distances; removes it from the list (order preserved) into rows_next.
@@ -292,6 +290,150 @@ __global__ void __launch_bounds__(256) bulyan_pick_kernel(const double* __restri
   __syncthreads();
   const int p = pick < 0 ? 0 : pick;
   for (int r = threadIdx.x; r < nr - 1; r += blockDim.x) rows_next[r] = rows[r < p ? r : r + 1];
+}
+
+// ---------------------------------------------------------------------------
+// Rounds with more than 128 remaining clients (N up to kBigMaxClients): two
+// passes per round instead of the fused one.
+//   select_rows_lds_kernel: a tile of `tile` coordinates x pn slots (pn =
+//     next_pow2(nr), [slot][coordinate] so a wave's compare-exchanges hit
+//     distinct banks) filled through the row list, bitonic-sorted by the
+//     whole workgroup (NaN-last order, padding NaN), then one lane per
+//     coordinate forms the round's aggregate exactly as the register kernel
+//     does (numpy's median / the ascending sequential fp32 window sum).
+//   dist_rows_kernel: the listed rows' squared distances to that aggregate
+//     with the fused kernel's arithmetic -- fp32 fma chains over the two
+//     32-coordinate halves of each wave, the four waves added in order, fp32
+//     across a block's tiles, the same per-block partial table for
+//     bulyan_dist_reduce_kernel -- so the pick sees the same distances
+//     whichever path a round took.
+// Row indices are clamped to the matrix (a bad list cannot fault).
+// ---------------------------------------------------------------------------
+constexpr int kBigMaxClients = 512;
+constexpr int kBigLdsFloats = 16384;   // 64 KiB tile
+
+__global__ void __launch_bounds__(256) select_rows_lds_kernel(const float* __restrict__ X, int64_t ldx,
+                                                              const int* __restrict__ rows, int nrows_x, int n, int pn,
+                                                              int tile, int64_t d, int median, int lo, int hi,
+                                                              float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * tile;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < pn * tile; e += blockDim.x) {
+    const int r = e / tile, c = e - r * tile;
+    const int64_t j = j0 + c;
+    float x = qnan();
+    if (r < n && j < d) {
+      const unsigned row = min(static_cast<unsigned>(rows[r]), static_cast<unsigned>(nrows_x - 1));
+      x = X[static_cast<int64_t>(row) * ldx + j];
+    }
+    lds[e] = x;
+  }
+  __syncthreads();
+  const int pairs = (pn / 2) * tile;
+  for (int k = 2; k <= pn; k <<= 1) {
+    for (int s = k >> 1; s > 0; s >>= 1) {
+      for (int q = tid; q < pairs; q += blockDim.x) {
+        const int c = q % tile;
+        const int h = q / tile;
+        const int i = ((h / s) * (2 * s)) + (h % s);
+        const int l = i + s;
+        float a = lds[i * tile + c], b = lds[l * tile + c];
+        if ((i & k) == 0) ce(a, b); else ce(b, a);
+        lds[i * tile + c] = a;
+        lds[l * tile + c] = b;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid < tile) {
+    const int64_t j = j0 + tid;
+    if (j < d) {
+      float res;
+      if (median) {   // np.median: NaN anywhere -> NaN (NaN sorts last, so slot n-1 is NaN)
+        if (n & 1) res = lds[((n - 1) / 2) * tile + tid];
+        else res = (lds[(n / 2 - 1) * tile + tid] + lds[(n / 2) * tile + tid]) * 0.5f;
+        if (__builtin_isnan(lds[(n - 1) * tile + tid])) res = qnan();
+      } else {        // window [lo, hi) of the sorted column, summed in ascending order
+        float acc = 0.f;
+        for (int p = lo; p < hi; ++p) acc += lds[p * tile + tid];
+        res = acc / static_cast<float>(hi - lo);
+      }
+      out[j] = res;
+    }
+  }
+}
+
+template <int MAXR>   // rows per thread-slot bound: nr <= 256 * MAXR
+__global__ void __launch_bounds__(256) dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
+                                                        const int* __restrict__ rows, int nrows_x, int nr, int64_t d,
+                                                        const float* __restrict__ agg, float* __restrict__ bpart,
+                                                        int nb, int tpb) {
+  const unsigned t = threadIdx.x;
+  const unsigned lane = t & 63u;
+  const unsigned w = t >> 6;
+  __shared__ float dl[4][32][68];
+  __shared__ float wsum[4][256 * MAXR];
+  float bs[MAXR];
+#pragma unroll
+  for (int q = 0; q < MAXR; ++q) bs[q] = 0.f;
+  const int64_t ntiles = cdiv(d, 256);
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * tpb;
+  const int64_t t1 = t0 + tpb < ntiles ? t0 + tpb : ntiles;
+  const unsigned ti = lane & 31u, th = lane >> 5;
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    const int64_t base = tile * 256;
+    const int64_t rem = d - base;
+    const bool valid = static_cast<int64_t>(t) < rem;
+    const int64_t j = valid ? base + t : d - 1;
+    const float a = agg[j];
+    for (int c = 0; 32 * c < nr; ++c) {
+      // this chunk's 32 row indices, loaded by the whole wave (full exec) and
+      // broadcast by readlane right here
+      const int li = 32 * c + static_cast<int>(lane & 31u);
+      const int rv = static_cast<int>(
+          min(static_cast<unsigned>(rows[li < nr ? li : nr - 1]), static_cast<unsigned>(nrows_x - 1)));
+      float xs[32];
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const int row = __builtin_amdgcn_readlane(rv, i);
+        xs[i] = X[static_cast<int64_t>(row) * ldx + j];
+      }
+#pragma unroll
+      for (int i = 0; i < 32; ++i) dl[w][i][lane] = valid ? a - xs[i] : 0.f;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float sh = 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(&dl[w][ti][32 * th + 4 * u]);
+        sh = __builtin_fmaf(q[0], q[0], sh);
+        sh = __builtin_fmaf(q[1], q[1], sh);
+        sh = __builtin_fmaf(q[2], q[2], sh);
+        sh = __builtin_fmaf(q[3], q[3], sh);
+      }
+      const float so = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(static_cast<int>((lane ^ 32u) * 4u),
+                                                                              __builtin_bit_cast(int, sh)));
+      const float st = th == 0 ? sh + so : so + sh;
+      if (th == 0 && 32 * c + static_cast<int>(ti) < nr) wsum[w][32 * c + ti] = st;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < MAXR; ++q) {
+      const int r = static_cast<int>(t) + 256 * q;
+      if (r < nr) bs[q] += (wsum[0][r] + wsum[1][r]) + (wsum[2][r] + wsum[3][r]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < MAXR; ++q) {
+    const int r = static_cast<int>(t) + 256 * q;
+    if (r < nr) bpart[static_cast<int64_t>(r) * nb + blockIdx.x] = bs[q];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -692,6 +834,138 @@ __global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(cons
   }
 }
 
+// ---------------------------------------------------------------------------
+// The stage for theta in (128, kBigMaxClients]: a 64-coordinate tile of pn =
+// next_pow2(theta) slots in LDS per 256-thread block, filled in selection
+// order through the row list, bitonic-sorted by the block; then one lane per
+// coordinate runs the register kernel's logic on its sorted column: the
+// exact-span test (every partial sum of <= theta values and |differences|
+// exact in fp64: 2 theta max|x| / ulp(min nonzero |x|) <= 2^53), the windows
+// of the centre candidates by bisection, the even-theta tie decided by the
+// first selection-order index holding either middle value (re-read from
+// global memory).  NaN / inf columns and inexact ones are listed for
+// bulyan_listed_big_kernel (the stage by definition).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) bulyan_final_lds_kernel(const float* __restrict__ S, int64_t lds_,
+                                                               const int* __restrict__ rows, int nrows_s, int theta,
+                                                               int pn, int keep, int64_t d, double* __restrict__ out,
+                                                               int* __restrict__ nf_count,
+                                                               int64_t* __restrict__ nf_list) {
+  extern __shared__ __attribute__((aligned(16))) float colt[];   // [pn][64]
+  __shared__ unsigned mnb_s[64], mxb_s[64];
+  __shared__ int nonfin_s[64];
+  const int tid = threadIdx.x;
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * 64;
+  if (tid < 64) {
+    mnb_s[tid] = 0xffffffffu;
+    mxb_s[tid] = 0u;
+    nonfin_s[tid] = 0;
+  }
+  __syncthreads();
+  for (int e = tid; e < pn * 64; e += blockDim.x) {
+    const int p = e >> 6, c = e & 63;
+    const int64_t j = j0 + c;
+    float x = __builtin_inff();
+    if (p < theta && j < d) {
+      const unsigned row = min(static_cast<unsigned>(rows[p]), static_cast<unsigned>(nrows_s - 1));
+      x = S[static_cast<int64_t>(row) * lds_ + j];
+      if (!__builtin_isfinite(x)) {
+        atomicOr(&nonfin_s[c], 1);
+        x = __builtin_isnan(x) ? __builtin_inff() : x;
+      } else {
+        const unsigned ab = __builtin_bit_cast(unsigned, x) & 0x7fffffffu;
+        if (ab != 0u) atomicMin(&mnb_s[c], ab);
+        atomicMax(&mxb_s[c], ab);
+      }
+    }
+    colt[e] = x;
+  }
+  __syncthreads();
+  const int pairs = (pn / 2) * 64;
+  for (int k = 2; k <= pn; k <<= 1) {
+    for (int s = k >> 1; s > 0; s >>= 1) {
+      for (int q = tid; q < pairs; q += blockDim.x) {
+        const int c = q & 63;
+        const int h = q >> 6;
+        const int i = ((h / s) * (2 * s)) + (h % s);
+        const int l = i + s;
+        float a = colt[i * 64 + c], b = colt[l * 64 + c];
+        if ((i & k) == 0) ce(a, b); else ce(b, a);
+        colt[i * 64 + c] = a;
+        colt[l * 64 + c] = b;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid >= 64) return;
+  const int64_t j = j0 + tid;
+  if (j >= d) return;
+  if (keep == 0) {   // the mean of an empty slice
+    out[j] = __builtin_nan("");
+    return;
+  }
+  if (nonfin_s[tid]) {
+    nf_list[atomicAdd(nf_count, 1)] = 2 * j + 1;
+    return;
+  }
+  bool exact = true;
+  if (mnb_s[tid] != 0xffffffffu) {
+    const int emx = static_cast<int>(mxb_s[tid] >> 23) - 126;   // max|x| < 2^emx
+    const int ebn = static_cast<int>(mnb_s[tid] >> 23);
+    const int ulp = (ebn > 0 ? ebn : 1) - 150;                   // ulp(min nonzero |x|) = 2^ulp
+    int lg = 0;
+    while ((1 << lg) < 2 * theta) ++lg;
+    exact = (emx + lg) - ulp <= 53;
+  }
+  if (!exact) {
+    nf_list[atomicAdd(nf_count, 1)] = 2 * j;
+    return;
+  }
+  auto s = [&](int p) -> float { return colt[p * 64 + tid]; };
+  const bool even = (theta & 1) == 0;
+  const int pl = even ? theta / 2 - 1 : (theta - 1) / 2;
+  const float cl = s(pl), cu = s(theta / 2);
+  double res = bulyan_window_mean(s, theta, keep, pl);
+  if (even && cu != cl) {
+    // exact totals tie: np.argmin takes the first selection-order index
+    // holding either middle value
+    const double res_u = bulyan_window_mean(s, theta, keep, theta / 2);
+    for (int p = 0; p < theta; ++p) {
+      const unsigned row = min(static_cast<unsigned>(rows[p]), static_cast<unsigned>(nrows_s - 1));
+      const float x = S[static_cast<int64_t>(row) * lds_ + j];
+      if (x == cl) break;
+      if (x == cu) {
+        res = res_u;
+        break;
+      }
+    }
+  }
+  out[j] = res;
+}
+
+// Listed columns of the big stage: the stage by definition
+// (bulyan_stage_generic), one lane per column, the rank map in LDS.
+__global__ void __launch_bounds__(32) bulyan_listed_big_kernel(const float* __restrict__ S, int64_t lds_,
+                                                               const int* __restrict__ rows, int nrows_s, int theta,
+                                                               int keep, const int* __restrict__ nf_count,
+                                                               const int64_t* __restrict__ nf_list,
+                                                               double* __restrict__ out) {
+  extern __shared__ int rank_slots[];   // [theta][32]
+  const int t = threadIdx.x;
+  const int cnt = *nf_count;
+  for (int e = blockIdx.x * 32 + t; e < cnt; e += gridDim.x * 32) {
+    const int64_t j = nf_list[e] >> 1;
+    auto a = [&](int i) -> double {
+      const unsigned row = min(static_cast<unsigned>(rows[i]), static_cast<unsigned>(nrows_s - 1));
+      return S[static_cast<int64_t>(row) * lds_ + j];
+    };
+    int m;
+    out[j] = keep == 0 ? __builtin_nan("")
+                       : bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return rank_slots[p * 32 + t]; },
+                                              &m);
+  }
+}
+
 // arr[np.argsort(distances)[:beta]] keeps min(beta, theta) values for beta >= 0
 // and max(theta + beta, 0) for beta < 0 (Python slice semantics,
 // robust_estimator.py:274; torch slicing at src/DBA/helper.py:939 likewise)
@@ -764,14 +1038,34 @@ static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int 
   return SRA_ERR_UNSUPPORTED;
 }
 
-static int launch_final(const float* S, int64_t lds_, const int* rows, int theta, int beta, int64_t d, double* out,
-                        int* nf_count, int64_t* nf_list, hipStream_t s) {
+static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows_s, int theta, int beta, int64_t d,
+                        double* out, int* nf_count, int64_t* nf_list, hipStream_t s) {
   const int keep = bulyan_keep(theta, beta);
   const int64_t blocks = cdiv(d, 256);
   const int P = static_cast<int>(cdiv(theta, 16) * 16);
-  SRA_REQUIRE(theta >= 1 && theta <= kFinalMaxTheta, SRA_ERR_UNSUPPORTED,
-              "bulyan per-coordinate stage supports theta <= %d (got %d)", kFinalMaxTheta, theta);
+  SRA_REQUIRE(theta >= 1 && theta <= kBigMaxClients, SRA_ERR_UNSUPPORTED,
+              "bulyan per-coordinate stage supports theta <= %d (got %d)", kBigMaxClients, theta);
   SRA_HIP(hipMemsetAsync(nf_count, 0, sizeof(int), s));
+  if (theta > kFinalMaxTheta) {
+    const int pn = next_pow2(theta);
+    const size_t lds_bytes = sizeof(float) * static_cast<size_t>(pn) * 64;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(bulyan_final_lds_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       static_cast<int>(sizeof(float) * kBigMaxClients * 64));
+    SRA_REQUIRE(attr == hipSuccess, SRA_ERR_UNSUPPORTED, "bulyan_final_lds_kernel: cannot reserve %zu bytes of LDS",
+                sizeof(float) * kBigMaxClients * 64);
+    hipLaunchKernelGGL(bulyan_final_lds_kernel, dim3(cdiv(d, 64)), dim3(256), lds_bytes, s, S, lds_, rows, nrows_s,
+                       theta, pn, keep, d, out, nf_count, nf_list);
+    int rc = launch_status("bulyan_final_lds_kernel");
+    if (rc) return rc;
+    static const hipError_t attr_l = hipFuncSetAttribute(reinterpret_cast<const void*>(bulyan_listed_big_kernel),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                         static_cast<int>(sizeof(int) * kBigMaxClients * 32));
+    SRA_REQUIRE(attr_l == hipSuccess, SRA_ERR_UNSUPPORTED, "bulyan_listed_big_kernel: cannot reserve its LDS");
+    hipLaunchKernelGGL(bulyan_listed_big_kernel, dim3(256), dim3(32), sizeof(int) * static_cast<size_t>(theta) * 32, s,
+                       S, lds_, rows, nrows_s, theta, keep, nf_count, nf_list, out);
+    return launch_status("bulyan_listed_big_kernel");
+  }
   int rc = SRA_ERR_UNSUPPORTED;
 #define SRA_FIN(PP)                                                                                              \
   case PP:                                                                                                       \
@@ -797,8 +1091,29 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int theta
 // order), both from ONE pass over the rows.  Over a column shard, dist is this
 // shard's share: the shards' dist vectors sum (all-reduce) to the distance
 // over all columns.  bpart: nr x round_blocks(d) floats.
-static int launch_bulyan_round(const float* X, int64_t d, int64_t ldx, const int* rows, int nr, int mode, bool dba,
-                               float* agg, float* bpart, double* dist, hipStream_t s) {
+static int launch_round_big(const float* X, int64_t ldx, const int* rows, int nrows_x, int nr, int64_t d, bool median,
+                            int lo, int hi, float* agg, float* bpart, hipStream_t s) {
+  SRA_REQUIRE(nr <= kBigMaxClients, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= %d (got %d)",
+              kBigMaxClients, nr);
+  const int pn = next_pow2(nr);
+  const int tile = kBigLdsFloats / pn;
+  hipLaunchKernelGGL(select_rows_lds_kernel, dim3(cdiv(d, tile)), dim3(256), sizeof(float) * pn * tile, s, X, ldx,
+                     rows, nrows_x, nr, pn, tile, d, median ? 1 : 0, lo, hi, agg);
+  int rc = launch_status("select_rows_lds_kernel");
+  if (rc) return rc;
+  const int64_t tpb = round_tiles_per_block(d);
+  const int64_t blocks = round_blocks(d);
+  if (nr <= 256)
+    hipLaunchKernelGGL(dist_rows_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, rows, nrows_x, nr, d, agg, bpart,
+                       static_cast<int>(blocks), static_cast<int>(tpb));
+  else
+    hipLaunchKernelGGL(dist_rows_kernel<2>, dim3(blocks), dim3(256), 0, s, X, ldx, rows, nrows_x, nr, d, agg, bpart,
+                       static_cast<int>(blocks), static_cast<int>(tpb));
+  return launch_status("dist_rows_kernel");
+}
+
+static int launch_bulyan_round(const float* X, int nrows_x, int64_t d, int64_t ldx, const int* rows, int nr, int mode,
+                               bool dba, float* agg, float* bpart, double* dist, hipStream_t s) {
   int lo, hi, sel_mode;
   if (mode == kBulyanMedian && dba) {
     lo = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
@@ -815,7 +1130,9 @@ static int launch_bulyan_round(const float* X, int64_t d, int64_t ldx, const int
     sel_mode = 1;
   }
   int rc;
-  if (sel_mode == 0)
+  if (nr > 128)
+    rc = launch_round_big(X, ldx, rows, nrows_x, nr, d, sel_mode == 0, lo, hi, agg, bpart, s);
+  else if (sel_mode == 0)
     rc = launch_select_dist<0>(X, ldx, rows, nr, d, lo, hi, agg, bpart, s);
   else
     rc = launch_select_dist<1>(X, ldx, rows, nr, d, lo, hi, agg, bpart, s);
@@ -855,9 +1172,10 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
     rc = launch_krum(X, n, d, ldx, dba ? f + 1 : f, theta, order, nullptr, rest, krum_workspace_bytes(n, d), s);
     if (rc) return rc;
     if (sel_out) SRA_HIP(hipMemcpyAsync(sel_out, order, sizeof(int) * theta, hipMemcpyDeviceToDevice, s));
-    return launch_final(X, ldx, order, theta, beta, d, out, nf_count, nf_list, s);
+    return launch_final(X, ldx, order, n, theta, beta, d, out, nf_count, nf_list, s);
   }
-  SRA_REQUIRE(n <= 128, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= 128 (got %d)", n);
+  SRA_REQUIRE(n <= kBigMaxClients, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= %d (got %d)",
+              kBigMaxClients, n);
   float* S = reinterpret_cast<float*>(rest);
   float* bpart = reinterpret_cast<float*>(
       (reinterpret_cast<uintptr_t>(S + static_cast<size_t>(theta) * static_cast<size_t>(d)) + 255) &
@@ -873,7 +1191,7 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   for (int t = 0; t < theta; ++t) {
     const int nr = n - t;
     float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
-    rc = launch_bulyan_round(X, d, ldx, cur, nr, mode, dba, agg, bpart, dist, s);
+    rc = launch_bulyan_round(X, n, d, ldx, cur, nr, mode, dba, agg, bpart, dist, s);
     if (rc) return rc;
     hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, dist, cur, nr, nxt, status);
     rc = launch_status("bulyan_pick_kernel");
@@ -882,7 +1200,7 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
     cur = nxt;
     nxt = tmp;
   }
-  return launch_final(S, d, order, theta, beta, d, out, nf_count, nf_list, s);
+  return launch_final(S, d, order, theta, theta, beta, d, out, nf_count, nf_list, s);
 }
 
 }  // namespace sra
@@ -899,7 +1217,8 @@ extern "C" int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32
 extern "C" int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode,
                               double* out, int32_t* selected, void* ws, size_t ws_bytes, void* stream) {
   SRA_REQUIRE(X != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
-  SRA_REQUIRE(n >= 1 && n <= 256 && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= 256)");
+  SRA_REQUIRE(n >= 1 && n <= kBigMaxClients && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= %d)",
+              kBigMaxClients);
   return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
                        static_cast<hipStream_t>(stream));
 }
@@ -907,7 +1226,8 @@ extern "C" int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx,
 extern "C" int sra_bulyan_dba_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode,
                                   double* out, int32_t* selected, void* ws, size_t ws_bytes, void* stream) {
   SRA_REQUIRE(X != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
-  SRA_REQUIRE(n >= 1 && n <= 256 && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= 256)");
+  SRA_REQUIRE(n >= 1 && n <= kBigMaxClients && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= %d)",
+              kBigMaxClients);
   SRA_REQUIRE(!(mode == kBulyanKrum && f == 1), SRA_ERR_ARG,
               "DBA bulyan_krum with f = 1 (its last round scores an empty neighbour set) is not supported");
   return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
@@ -932,8 +1252,8 @@ extern "C" int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t
 // selections made elsewhere (a d-sharded Bulyan, a caller's own rounds).
 extern "C" int sra_bulyan_stage_workspace_bytes(int64_t theta, int64_t d, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
-  SRA_REQUIRE(theta >= 1 && theta <= kFinalMaxTheta && d >= 1, SRA_ERR_SHAPE, "need 1 <= theta <= %d, d >= 1",
-              kFinalMaxTheta);
+  SRA_REQUIRE(theta >= 1 && theta <= kBigMaxClients && d >= 1, SRA_ERR_SHAPE, "need 1 <= theta <= %d, d >= 1",
+              kBigMaxClients);
   *bytes = 256 + (static_cast<size_t>(theta) * sizeof(int) + 255) / 256 * 256 + sizeof(int64_t) * static_cast<size_t>(d);
   return SRA_OK;
 }
@@ -941,8 +1261,8 @@ extern "C" int sra_bulyan_stage_workspace_bytes(int64_t theta, int64_t d, size_t
 extern "C" int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, int64_t lds, int32_t beta, double* out,
                                     void* ws, size_t ws_bytes, void* stream) {
   SRA_REQUIRE(S != nullptr && out != nullptr && ws != nullptr, SRA_ERR_ARG, "null pointer");
-  SRA_REQUIRE(theta >= 1 && theta <= kFinalMaxTheta, SRA_ERR_UNSUPPORTED, "1 <= theta <= %d (got %lld)",
-              kFinalMaxTheta, static_cast<long long>(theta));
+  SRA_REQUIRE(theta >= 1 && theta <= kBigMaxClients, SRA_ERR_UNSUPPORTED, "1 <= theta <= %d (got %lld)",
+              kBigMaxClients, static_cast<long long>(theta));
   SRA_REQUIRE(d >= 1 && lds >= d, SRA_ERR_SHAPE, "bad d / lds");
   size_t need = 0;
   sra_bulyan_stage_workspace_bytes(theta, d, &need);
@@ -955,15 +1275,17 @@ extern "C" int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, in
   hipLaunchKernelGGL(iota_kernel, dim3(cdiv(theta, 256)), dim3(256), 0, s, rows, static_cast<int>(theta));
   const int rc = launch_status("iota_kernel");
   if (rc) return rc;
-  return launch_final(S, lds, rows, static_cast<int>(theta), beta, d, out, nf_count, nf_list, s);
+  return launch_final(S, lds, rows, static_cast<int>(theta), static_cast<int>(theta), beta, d, out, nf_count, nf_list,
+                      s);
 }
 
 // One Bulyan selection round over a (possibly column-sharded) N x d block, for
 // a caller that sums the shards' distances (all-reduce) and picks itself.
 extern "C" int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
-  SRA_REQUIRE(n >= 1 && n <= 128, SRA_ERR_UNSUPPORTED, "bulyan rounds support 1 <= N <= 128");
-  *bytes = kRoundPartialMaxBytes + 256;
+  SRA_REQUIRE(n >= 1 && n <= kBigMaxClients, SRA_ERR_UNSUPPORTED, "bulyan rounds support 1 <= N <= %d",
+              kBigMaxClients);
+  *bytes = sizeof(float) * static_cast<size_t>(n) * kRoundMaxBlocks + 256;
   return SRA_OK;
 }
 
@@ -972,15 +1294,15 @@ extern "C" int sra_bulyan_round_f32(const float* X, int64_t n, int64_t d, int64_
                                     size_t ws_bytes, void* stream) {
   SRA_REQUIRE(X != nullptr && rows != nullptr && agg != nullptr && dist != nullptr && ws != nullptr, SRA_ERR_ARG,
               "null pointer");
-  SRA_REQUIRE(n >= 1 && n <= 128 && nr >= 1 && nr <= n && d >= 1 && ldx >= d, SRA_ERR_SHAPE,
-              "bad shape (N <= 128, 1 <= nr <= N)");
+  SRA_REQUIRE(n >= 1 && n <= kBigMaxClients && nr >= 1 && nr <= n && d >= 1 && ldx >= d, SRA_ERR_SHAPE,
+              "bad shape (N <= %d, 1 <= nr <= N)", kBigMaxClients);
   SRA_REQUIRE(mode == kBulyanMedian || mode == kBulyanTrimmed, SRA_ERR_ARG, "round mode must be median (1) or "
               "trimmedmean (2), got %d", mode);
   size_t need = 0;
   sra_bulyan_round_workspace_bytes(n, &need);
   SRA_REQUIRE(ws_bytes >= need, SRA_ERR_WORKSPACE, "bulyan round workspace too small: need %zu bytes", need);
-  return launch_bulyan_round(X, d, ldx, rows, nr, mode, dba != 0, agg, static_cast<float*>(ws), dist,
-                             static_cast<hipStream_t>(stream));
+  return launch_bulyan_round(X, static_cast<int>(n), d, ldx, rows, nr, mode, dba != 0, agg, static_cast<float*>(ws),
+                             dist, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int sra_bulyan_pick(const double* dist, const int32_t* rows, int32_t nr, int32_t* rows_next,

@@ -547,17 +547,20 @@ __device__ __attribute__((noinline)) void tri_top(double* trw, int m, double tsc
 // Once per filter iteration, so it is kept out of line: the solver's 64 Gram
 // registers per lane stay put while this runs.  Returns false when no
 // candidate is feasible.  Block-wide (all 256 lanes), barriers inside.
-__device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int row, bool own, int nk, double cap,
-                                                     double* cvec, double* vscr, int* ibuf, double* red,
-                                                     double* hbuf, int* capped) {
+// NP: row capacity of the scratch, NW: waves of the block (needs red[NW],
+// ibuf[3 NP + 2 NW], vscr[3 NP]).
+template <int NP, int NW>
+__device__ __attribute__((noinline)) bool kl_project_t(double* ci_io, bool ai, int row, bool own, int nk, double cap,
+                                                       double* cvec, double* vscr, int* ibuf, double* red,
+                                                       double* hbuf, int* capped) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int* kidx = ibuf;            // compact -> client row
-  int* irank = ibuf + FNP;     // descending rank of a compact entry
-  int* flag = ibuf + 2 * FNP;  // active flags
-  int* islot = ibuf + 3 * FNP; // argmax indices
+  int* irank = ibuf + NP;      // descending rank of a compact entry
+  int* flag = ibuf + 2 * NP;   // active flags
+  int* islot = ibuf + 3 * NP;  // argmax indices
   double* cc = vscr;           // compact weights
-  double* sv = vscr + FNP;     // weights in descending order
-  double* hl = vscr + 2 * FNP; // sv * log(sv / cap)
+  double* sv = vscr + NP;      // weights in descending order
+  double* hl = vscr + 2 * NP;  // sv * log(sv / cap)
   const double ci = *ci_io;
   if (own) flag[row] = ai ? 1 : 0;
   __syncthreads();
@@ -604,7 +607,7 @@ __device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int
   if (lane == 0) islot[wave] = stop;
   __syncthreads();
   int istop = islot[0];
-  for (int q2 = 1; q2 < 4; ++q2) istop = islot[q2] < istop ? islot[q2] : istop;
+  for (int q2 = 1; q2 < NW; ++q2) istop = islot[q2] < istop ? islot[q2] : istop;
   if (tid >= istop) negkl = -__builtin_inf();
   double v = negkl;
   int bi = tid;
@@ -619,15 +622,15 @@ __device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int
   }
   if (lane == 0) {
     red[wave] = v;
-    islot[4 + wave] = bi;
+    islot[NW + wave] = bi;
   }
   __syncthreads();
   double bv = red[0];
-  bi = islot[4];
-  for (int q2 = 1; q2 < 4; ++q2)
-    if (red[q2] > bv || (red[q2] == bv && islot[4 + q2] < bi)) {
+  bi = islot[NW];
+  for (int q2 = 1; q2 < NW; ++q2)
+    if (red[q2] > bv || (red[q2] == bv && islot[NW + q2] < bi)) {
       bv = red[q2];
-      bi = islot[4 + q2];
+      bi = islot[NW + q2];
     }
   const bool ok = bv > -__builtin_inf();
   *capped = ok ? bi + 1 : 0;
@@ -637,6 +640,10 @@ __device__ __attribute__((noinline)) bool kl_project(double* ci_io, bool ai, int
   __syncthreads();
   if (ok && ai) *ci_io = cvec[row];
   return ok;
+}
+__device__ __forceinline__ bool kl_project(double* ci_io, bool ai, int row, bool own, int nk, double cap, double* cvec,
+                                           double* vscr, int* ibuf, double* red, double* hbuf, int* capped) {
+  return kl_project_t<FNP, 4>(ci_io, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf, capped);
 }
 
 // MODE 0: filterL2, 1: ex_noregret; DBG: diagnostics of chunk 0.  Since round
@@ -2037,19 +2044,544 @@ __global__ void list_all_kernel(int* list, int* count, int nb) {
 __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
                                                          int itv, int64_t chunk0, int nb,
                                                          const double* __restrict__ c, const int* __restrict__ act,
-                                                         const double* __restrict__ misc, double* __restrict__ out) {
+                                                         const double* __restrict__ misc, double* __restrict__ out,
+                                                         int cs) {
   const int64_t j0 = chunk0 * itv;
   const int64_t jend = (chunk0 + nb) * static_cast<int64_t>(itv);
   const int64_t j1 = jend < d ? jend : d;
   const int64_t j = j0 + static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (j >= j1) return;
   const int b = static_cast<int>((j - j0) / itv);
-  const double* cb = c + static_cast<size_t>(b) * FNP;
-  const int* ab = act + static_cast<size_t>(b) * FNP;
+  const double* cb = c + static_cast<size_t>(b) * cs;
+  const int* ab = act + static_cast<size_t>(b) * cs;
   double s = 0.0;
   for (int i = 0; i < n; ++i)
     if (ab[i]) s += static_cast<double>(X[static_cast<int64_t>(i) * ldx + j]) * cb[i];
   out[j] = s / misc[static_cast<size_t>(b) * kMisc];
+}
+
+// ============================================================================
+// N in (128, NBIG]: the same filters with the client-space objects out of
+// registers (the reference has no client limit, robust_estimator.py:42-218).
+//   chunk_colmean_kernel + chunk_gram_big_kernel: the centred chunk Gram on the
+//     fp64 MFMA in 64 x 64 output blocks (each block stages its two row blocks
+//     through LDS and centres them by the chunk's fp64 column means);
+//   noregret_pre_big_kernel: ex_noregret's Krum pre-filter, one wave per
+//     distance row, the row bitonic-sorted in the wave's LDS slice;
+//   filter_big_kernel<MODE>: filter_solve_kernel's re-orthogonalising Lanczos
+//     with G read from global memory (column i of the symmetric G: coalesced),
+//     the basis in a per-workgroup global slot (each entry read back only by
+//     the thread that wrote it), 1024 threads = two per client row (the two
+//     halves of every matvec).
+// A correctness path: the BASELINE configurations all have N <= 128 per
+// filter (C5 filters 128 bucket means).
+// ============================================================================
+constexpr int NBIG = 512;
+constexpr int kBigThreads = 1024;
+constexpr int kBigWaves = kBigThreads / 64;
+constexpr int kBatchBig = 256;     // chunks per workspace batch
+constexpr int kBigGrid = 256;      // filter_big_kernel workgroups (one per CU), each owns a basis slot
+constexpr int kBigTile = 64;       // Gram output block
+
+__global__ void __launch_bounds__(256) chunk_colmean_kernel(const float* __restrict__ X, int n, int64_t d,
+                                                            int64_t ldx, int itv, int64_t chunk0, int nb,
+                                                            double* __restrict__ mu) {
+  const int64_t j0 = chunk0 * itv;
+  const int64_t jend = (chunk0 + nb) * static_cast<int64_t>(itv);
+  const int64_t j1 = jend < d ? jend : d;
+  const int64_t j = j0 + static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= j1) return;
+  double sm = 0.0;
+  for (int i = 0; i < n; ++i) sm += static_cast<double>(X[static_cast<int64_t>(i) * ldx + j]);
+  mu[j - j0] = sm / n;
+}
+
+// block (I, J), I <= J, of chunk blockIdx.y: wave w owns rows 16 w .. + 15 of
+// I against the four 16-row groups of J
+__global__ void __launch_bounds__(256) chunk_gram_big_kernel(const float* __restrict__ X, int n, int64_t d,
+                                                             int64_t ldx, int itv, int64_t chunk0,
+                                                             const double* __restrict__ mu, double* __restrict__ Gb) {
+  __shared__ __attribute__((aligned(16))) float sa[kBigTile * FROW];
+  __shared__ __attribute__((aligned(16))) float sb[kBigTile * FROW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.y;
+  int I = 0, J = 0;
+  {
+    const int nbk = static_cast<int>(cdiv(n, kBigTile));
+    int p = blockIdx.x;
+    while (p >= nbk - I) {
+      p -= nbk - I;
+      ++I;
+    }
+    J = I + p;
+  }
+  const int64_t k0 = (chunk0 + b) * static_cast<int64_t>(itv);
+  const int k = static_cast<int>((k0 + itv < d ? k0 + itv : d) - k0);
+  const double* mub = mu + static_cast<int64_t>(b) * itv;
+  f64x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int s0 = 0; s0 < k; s0 += FST) {
+    for (int e = tid; e < kBigTile * FST; e += 256) {
+      const int r = e / FST, cc = e - (e / FST) * FST;
+      const int ra = kBigTile * I + r, rb = kBigTile * J + r;
+      const bool okc = s0 + cc < k;
+      sa[r * FROW + cc] = (ra < n && okc) ? X[static_cast<int64_t>(ra) * ldx + k0 + s0 + cc] : 0.f;
+      sb[r * FROW + cc] = (rb < n && okc) ? X[static_cast<int64_t>(rb) * ldx + k0 + s0 + cc] : 0.f;
+    }
+    __syncthreads();
+    for (int ks = 0; ks < FST / 4; ++ks) {
+      const int cc = 4 * ks + (lane >> 4);
+      const double m = s0 + cc < k ? mub[s0 + cc] : 0.0;
+      const int ra = 16 * w + (lane & 15);
+      const double fa = (kBigTile * I + ra < n && s0 + cc < k) ? static_cast<double>(sa[ra * FROW + cc]) - m : 0.0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int rb = 16 * t + (lane & 15);
+        const double fb = (kBigTile * J + rb < n && s0 + cc < k) ? static_cast<double>(sb[rb * FROW + cc]) - m : 0.0;
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  double* G = Gb + static_cast<size_t>(b) * n * n;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      const int row = kBigTile * I + 16 * w + (lane >> 4) + 4 * rg;
+      const int col = kBigTile * J + 16 * t + (lane & 15);
+      if (row < n && col < n) {
+        G[static_cast<size_t>(row) * n + col] = acc[t][rg];
+        if (I != J) G[static_cast<size_t>(col) * n + row] = acc[t][rg];
+      }
+    }
+  }
+}
+
+// numpy pairwise fp32 sum of f(0..m), m <= 512 (two levels of splits)
+template <typename F>
+__device__ float np_pw32_big(int m, F&& f) {
+  auto blk = [&](int lo, int mm) -> float {
+    if (mm < 8) {
+      float r = 0.f;
+      for (int i = 0; i < mm; ++i) r += f(lo + i);
+      return r;
+    }
+    float r0 = f(lo), r1 = f(lo + 1), r2 = f(lo + 2), r3 = f(lo + 3), r4 = f(lo + 4), r5 = f(lo + 5),
+          r6 = f(lo + 6), r7 = f(lo + 7);
+    int i = 8;
+    for (; i < mm - (mm % 8); i += 8) {
+      r0 += f(lo + i); r1 += f(lo + i + 1); r2 += f(lo + i + 2); r3 += f(lo + i + 3);
+      r4 += f(lo + i + 4); r5 += f(lo + i + 5); r6 += f(lo + i + 6); r7 += f(lo + i + 7);
+    }
+    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < mm; ++i) res += f(lo + i);
+    return res;
+  };
+  auto half = [&](int lo, int mm) -> float {
+    if (mm <= 128) return blk(lo, mm);
+    int q = mm / 2;
+    q -= q % 8;
+    return blk(lo, q) + blk(lo + q, mm - q);
+  };
+  if (m <= 128) return blk(0, m);
+  int m2 = m / 2;
+  m2 -= m2 % 8;
+  return half(0, m2) + half(m2, m - m2);
+}
+
+__global__ void __launch_bounds__(kBigThreads) noregret_pre_big_kernel(const double* __restrict__ Gb, int n, double eps,
+                                                                       int* __restrict__ act, double* __restrict__ misc) {
+  __shared__ float srt[kBigWaves][NBIG];
+  __shared__ double diag[NBIG];
+  __shared__ double score[NBIG];
+  __shared__ int keep[NBIG];
+  __shared__ float red[kBigWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x;
+  const double* G = Gb + static_cast<size_t>(b) * n * n;
+  const int fp = static_cast<int>(ceil(eps * n));
+  if (tid < n) diag[tid] = G[static_cast<size_t>(tid) * n + tid];
+  __syncthreads();
+  auto dist = [&](int i, int j) -> float {
+    const double sq = diag[i] + diag[j] - 2.0 * G[static_cast<size_t>(i) * n + j];
+    return static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
+  };
+  const int m = n - fp - 2 >= 0 ? (n - fp - 2 < n - 1 ? n - fp - 2 : n - 1)
+                                : ((n - 1) + (n - fp - 2) > 0 ? (n - 1) + (n - fp - 2) : 0);
+  const int pn = next_pow2(n - 1 > 1 ? n - 1 : 1);
+  float* sr = srt[wave];
+  for (int row = wave; row < n; row += kBigWaves) {
+    for (int p = lane; p < pn; p += 64) sr[p] = p < n - 1 ? dist(row, p < row ? p : p + 1) : __builtin_inff();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int kk = 2; kk <= pn; kk <<= 1) {
+      for (int st = kk >> 1; st > 0; st >>= 1) {
+        for (int h = lane; h < pn / 2; h += 64) {
+          const int a = (h / st) * (2 * st) + (h % st);
+          const float va = sr[a], vb = sr[a + st];
+          const float lo = fminf(va, vb), hi = fmaxf(va, vb);
+          const bool up = (a & kk) == 0;
+          sr[a] = up ? lo : hi;
+          sr[a + st] = up ? hi : lo;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+    if (lane == 0) score[row] = static_cast<double>(np_pw32_big(m, [&](int q) { return sr[q]; }));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();
+  // argpartition(metric, -f)[:-f]: drop the fp largest (ties: the later index first)
+  if (tid < NBIG) {
+    int kp = 0;
+    if (tid < n) {
+      const double si = score[tid];
+      int above = 0;
+      for (int j = 0; j < n; ++j) above += (score[j] > si || (score[j] == si && j > tid)) ? 1 : 0;
+      kp = above >= fp ? 1 : 0;
+    }
+    keep[tid] = kp;
+    act[static_cast<size_t>(b) * NBIG + tid] = kp;
+  }
+  __syncthreads();
+  float md = 0.f;
+  for (int e = tid; e < n * n; e += kBigThreads) {
+    const int i = e / n, j = e - (e / n) * n;
+    if (i < j && keep[i] && keep[j]) {
+      const float dd = dist(i, j);
+      md = dd > md ? dd : md;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float o = __shfl_xor(md, off);
+    md = o > md ? o : md;
+  }
+  if (lane == 0) red[wave] = md;
+  __syncthreads();
+  if (tid == 0) {
+    float mx = red[0];
+    for (int q = 1; q < kBigWaves; ++q) mx = red[q] > mx ? red[q] : mx;
+    misc[static_cast<size_t>(b) * kMisc + 1] = static_cast<double>(0.5f / (mx * mx));
+  }
+}
+
+struct BigArgs {
+  const double* G;   // [nb][n][n]
+  double* c;         // [nb][NBIG]
+  int* act;          // [nb][NBIG]
+  double* misc;      // [nb][kMisc]
+  int* status;
+  int n;
+  int nb;
+  double eps;
+  double sigma;
+  double expansion;
+  double* Vg;        // [grid][LMAX][NBIG]
+  int* trace;        // optional [nb][1 + 2 n] decision trace (batch-relative), the small path's layout
+};
+
+constexpr int kHStride = LMAX + 2;
+constexpr size_t kBigLds =
+    sizeof(double) * (4 * NBIG + kBigWaves * kHStride + kHStride + 2 * 4 * kBigWaves + kBigWaves * TRI + 4 * NBIG) +
+    sizeof(int) * (3 * NBIG + 4 * kBigWaves + 16);
+static_assert(kBigLds <= 163840, "the big solver's LDS must fit one CU");
+
+template <int MODE>
+__global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* xbuf = reinterpret_cast<double*>(smem);   // [NBIG] operator input
+  double* ysum = xbuf + NBIG;                       // [2][NBIG] matvec halves
+  double* rbuf = ysum + 2 * NBIG;                   // [NBIG] scratch
+  double* hpart = rbuf + NBIG;                      // [kBigWaves][kHStride] per-wave dot products
+  double* hbuf = hpart + kBigWaves * kHStride;      // [kHStride] Gram-Schmidt coefficients (+ |r''|^2)
+  double* red = hbuf + kHStride;                    // [2][4 kBigWaves] block reductions
+  double* tri = red + 2 * 4 * kBigWaves;            // [kBigWaves][TRI] per-wave tridiagonal record
+  double* cvec = tri + kBigWaves * TRI;             // [NBIG]
+  double* vscr = cvec + NBIG;                       // [3][NBIG]
+  int* ibuf = reinterpret_cast<int*>(vscr + 3 * NBIG);   // [3][NBIG] + [4][kBigWaves] + [16]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = tid & (NBIG - 1);
+  const int half = tid >> 9;       // which half of every matvec's columns
+  const bool own = half == 0;      // the first 512 threads speak for their row
+  const int n = A.n;
+  double* trw = tri + wave * TRI;
+  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * LMAX * NBIG;
+
+  int rslot = 0;
+  auto reduce4 = [&](double v0, double v1, double v2, double v3, double (&o)[4], int nv) {
+    v0 = wave_sum(v0);
+    if (nv > 1) v1 = wave_sum(v1);
+    if (nv > 2) v2 = wave_sum(v2);
+    if (nv > 3) v3 = wave_sum(v3);
+    double* R = red + 4 * kBigWaves * rslot;
+    if (lane == 0) {
+      R[4 * wave + 0] = v0;
+      if (nv > 1) R[4 * wave + 1] = v1;
+      if (nv > 2) R[4 * wave + 2] = v2;
+      if (nv > 3) R[4 * wave + 3] = v3;
+    }
+    __syncthreads();
+    for (int kk = 0; kk < nv; ++kk) {
+      double acc = R[kk];
+      for (int q = 1; q < kBigWaves; ++q) acc += R[4 * q + kk];
+      o[kk] = acc;
+    }
+    rslot ^= 1;
+  };
+  auto argmax_first = [&](double v, int i, double* vbest) -> int {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ov = __shfl_xor(v, off);
+      const int oi = __shfl_xor(i, off);
+      if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+      }
+    }
+    double* R = red + 4 * kBigWaves * rslot;
+    int* I = ibuf + 3 * NBIG + 2 * kBigWaves * rslot;
+    if (lane == 0) {
+      R[wave] = v;
+      I[wave] = i;
+    }
+    __syncthreads();
+    double bv = R[0];
+    int bi = I[0];
+    for (int q = 1; q < kBigWaves; ++q)
+      if (R[q] > bv || (R[q] == bv && I[q] < bi)) {
+        bv = R[q];
+        bi = I[q];
+      }
+    rslot ^= 1;
+    *vbest = bv;
+    return bi;
+  };
+  // y_row = sum_j G[j][row] x_j (G symmetric): each half sums its columns in
+  // order, the halves are added in a fixed order
+  auto gmv = [&](const double* G) -> double {
+    const int hn = (n + 1) >> 1;
+    const int j0 = half * hn, j1 = j0 + hn < n ? j0 + hn : n;
+    double p0 = 0.0, p1 = 0.0;
+    if (row < n) {
+      int j = j0;
+      for (; j + 1 < j1; j += 2) {
+        p0 = fma(G[static_cast<size_t>(j) * n + row], xbuf[j], p0);
+        p1 = fma(G[static_cast<size_t>(j + 1) * n + row], xbuf[j + 1], p1);
+      }
+      if (j < j1) p0 = fma(G[static_cast<size_t>(j) * n + row], xbuf[j], p0);
+    }
+    // ysum is rewritten by the next gmv only after a reduction's barrier
+    ysum[half * NBIG + row] = p0 + p1;
+    __syncthreads();
+    return ysum[row] + ysum[NBIG + row];
+  };
+
+  for (int ch = blockIdx.x; ch < A.nb; ch += gridDim.x) {
+    const double* G = A.G + static_cast<size_t>(ch) * n * n;
+    bool ai;
+    if constexpr (MODE == 1) ai = own && row < n && A.act[static_cast<size_t>(ch) * NBIG + row] != 0;
+    else ai = own && row < n;
+    double ci = ai ? 1.0 : 0.0;
+    const int fdrop = static_cast<int>(ceil(A.eps * n));
+    const int n_keep = MODE == 1 ? n - (fdrop < n ? fdrop : n) : n;
+    const double step = MODE == 1 ? A.misc[static_cast<size_t>(ch) * kMisc + 1] : 0.0;
+    const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n) : static_cast<int>(2 * A.eps * n_keep);
+    double ui = 0.0;
+    bool have_u = false;
+    int m_hint = 12;
+    double rate_hint = 0.0;
+    int done = 0;
+    int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * (1 + 2 * n) : nullptr;
+
+    for (int it = 0; it < iters; ++it) {
+      double o[4];
+      reduce4(ai ? ci : 0.0, ai ? 1.0 : 0.0, 0.0, 0.0, o, 2);
+      const double csum = o[0];
+      const int nact = static_cast<int>(o[1]);
+      const double wi = ai ? ci / csum : 0.0;
+      const double swi = sqrt(wi > 0.0 ? wi : 0.0);
+      if (own) xbuf[row] = wi;
+      __syncthreads();
+      const double gwi = gmv(G);
+      reduce4(own ? wi * gwi : 0.0, 0.0, 0.0, 0.0, o, 1);
+      const double sgw = o[0];
+
+      double lam = 0.0;
+      int m_conv = 0, restarts = 0;
+      double rt;
+      {
+        const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
+        rt = swi > 0.0 ? (have_u ? ui + 1e-3 * swi * hh : swi * hh) : 0.0;
+      }
+      for (;;) {
+        double xt = swi * rt;
+        if (own) xbuf[row] = xt;
+        reduce4(own ? rt * rt : 0.0, own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, o, 3);
+        double nrm2 = o[0], S1 = o[1], GY = o[2];
+        double qprev = 0.0, tscale = 0.0, theta_lb = -1e300;
+        int next_check = m_hint - 1 > 4 ? m_hint - 1 : 4;
+        int m_a = -1;
+        double res_a = 0.0;
+        bool converged = false;
+        for (int j = 0;; ++j) {
+          const double bet = sqrt(nrm2);
+          if (j > 0) {
+            if (lane == 0) trw[64 + j - 1] = bet * bet;
+            tscale = fmax(tscale, bet);
+            const bool breakdown = !(bet > 1e-14 * tscale);
+            if (breakdown || j >= nact || j == LMAX || j >= next_check) {
+              const int m = j;
+              __builtin_amdgcn_wave_barrier();
+              double lm, zlast;
+              tri_top(trw, m, tscale, theta_lb, &lm, &zlast);
+              lam = lm;
+              const double resid = fabs(bet * zlast);
+              theta_lb = lm;
+              if (resid <= kResTol * fabs(lm) || breakdown || j >= nact) {
+                converged = true;
+                m_conv = m;
+                break;
+              }
+              if (j == LMAX) break;
+              int adv = 4;
+              double rate = rate_hint;
+              if (m_a >= 0 && res_a > resid && resid > 0.0) rate = rate_hint = log(resid / res_a) / (m - m_a);
+              if (rate < 0.0 && resid > 0.0) {
+                const double need = log(kResTol * fabs(lm) / resid) / rate;
+                adv = need < 1.0 ? 1 : (need > LMAX ? LMAX : static_cast<int>(ceil(need)));
+              }
+              m_a = m;
+              res_a = resid;
+              next_check = m + adv;
+            }
+          }
+          // (1) y = G x~, alpha_j, r' = M q_j - beta q_{j-1}
+          const double y = gmv(G);
+          const double cx = y - gwi * S1 - GY + sgw * S1;
+          const double ib = 1.0 / bet;
+          const double q = rt * ib;
+          if (own && row < n) Vb[static_cast<size_t>(j) * NBIG + row] = q;
+          const double rp = swi * cx * ib - (j > 0 ? bet * qprev : 0.0);
+          qprev = q;
+          reduce4(own ? swi * rt * y : 0.0, 0.0, 0.0, 0.0, o, 1);
+          const double aj = (o[0] - 2.0 * S1 * GY + sgw * S1 * S1) * (ib * ib);
+          double r = own && row < n ? rp - aj * q : 0.0;
+          double alpha = aj;
+#pragma unroll 1
+          for (int pass = 0; pass < 2; ++pass) {
+            // (2) h_q = q_q . r (q <= j), and |r|^2 in the first pass
+            const int nh = pass == 0 ? j + 2 : j + 1;
+            for (int qq = 0; qq < nh; ++qq) {
+              double v = 0.0;
+              if (own && row < n) v = qq <= j ? Vb[static_cast<size_t>(qq) * NBIG + row] * r : r * r;
+              v = wave_sum(v);
+              if (lane == 0) hpart[wave * kHStride + qq] = v;
+            }
+            __syncthreads();
+            if (tid < nh) {
+              double hs = hpart[tid];
+              for (int w2 = 1; w2 < kBigWaves; ++w2) hs += hpart[w2 * kHStride + tid];
+              hbuf[tid] = hs;
+            }
+            __syncthreads();
+            // (3) r -= sum_q h_q q_q
+            double upd = 0.0, hn2 = 0.0;
+            for (int qq = 0; qq <= j; ++qq) {
+              const double hv = hbuf[qq];
+              if (own && row < n) upd = fma(hv, Vb[static_cast<size_t>(qq) * NBIG + row], upd);
+              hn2 = fma(hv, hv, hn2);
+            }
+            r -= upd;
+            alpha += hbuf[j];
+            if (pass == 1) break;
+            const double rr2 = hbuf[j + 1];
+            if (!(rr2 - hn2 < kDgks * rr2)) break;
+            __syncthreads();   // hbuf is rewritten by the second pass
+          }
+          if (lane == 0) trw[j] = alpha;
+          tscale = fmax(tscale, fabs(alpha));
+          rt = r;
+          xt = swi * r;
+          if (own) xbuf[row] = xt;
+          reduce4(own ? r * r : 0.0, own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, o, 3);
+          nrm2 = o[0];
+          S1 = o[1];
+          GY = o[2];
+        }
+        {
+          const int m = converged ? m_conv : LMAX;
+          double u0 = 0.0;
+          if (own && row < n)
+            for (int qq = 0; qq < m; ++qq) u0 = fma(trw[128 + qq], Vb[static_cast<size_t>(qq) * NBIG + row], u0);
+          ui = u0;
+        }
+        if (converged || restarts == kMaxRestarts) break;
+        ++restarts;
+        rt = ui;
+        __syncthreads();
+      }
+      m_hint = m_conv > 4 ? m_conv : 4;
+      have_u = true;
+      if (lam * lam <= A.expansion * A.sigma * A.sigma) break;   // robust_estimator.py:163-164 / :71-72
+      {
+        const double xt = swi * ui;
+        if (own) xbuf[row] = xt;
+        reduce4(own ? xt : 0.0, own ? gwi * xt : 0.0, 0.0, 0.0, o, 2);
+      }
+      const double cu = gmv(G) - gwi * o[0] - o[1] + sgw * o[0];
+      const double ti = cu * cu / lam;
+      if constexpr (MODE == 0) {
+        double tmax = 0.0;
+        const int p = argmax_first(ai ? ti : -__builtin_inf(), row, &tmax);
+        const double cn = (ai && row != p) ? ci * (1.0 - ti / tmax) : 0.0;
+        reduce4(own ? fabs(cn) : 0.0, 0.0, 0.0, 0.0, o, 1);
+        ci = cn / o[0];
+        if (row == p) ai = false;
+        if (tr != nullptr && tid == 0) tr[1 + it] = p;
+      } else {
+        const int nk = n_keep;
+        const double cap = 1.0 / (1.0 - A.eps) / nk;
+        if (ai) ci = ci * (1.0 - step * ti);
+        int capped = 0;
+        if (!kl_project_t<NBIG, kBigWaves>(&ci, ai, row, own && row < n, nk, cap, cvec, vscr, ibuf, red, hbuf,
+                                            &capped)) {
+          if (tid == 0) *A.status = 2;
+          break;
+        }
+        if (tr != nullptr && tid == 0) tr[1 + it] = capped;
+      }
+      done = it + 1;
+    }
+    if (tr != nullptr) {
+      if (tid == 0) tr[0] = done;
+      if (own && row < n) tr[1 + n + row] = ai ? 1 : 0;
+    }
+    __syncthreads();
+    if (own) {
+      cvec[row] = ai ? ci : 0.0;
+      ibuf[2 * NBIG + row] = ai ? 1 : 0;
+      A.c[static_cast<size_t>(ch) * NBIG + row] = ai ? ci : 0.0;
+      A.act[static_cast<size_t>(ch) * NBIG + row] = ai ? 1 : 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int q2 = 0;
+      double* kept = vscr;
+      for (int i = 0; i < n; ++i)
+        if (ibuf[2 * NBIG + i]) kept[q2++] = cvec[i];
+      A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int z) { return kept[z]; });
+    }
+    __syncthreads();
+  }
 }
 
 // ============================================================================
@@ -2059,7 +2591,70 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
 constexpr size_t kChunkWsBytes = sizeof(double) * (FNP * FNP + FNP + kMisc) + sizeof(int) * (FNP + 1);
 constexpr int kLanczosGrid = 512;    // workgroups of lanczos_solve_kernel: 2 per CU, each owns a basis slot
 
-size_t filter_workspace_bytes(int64_t d, int itv) {
+// N > FNP: [G nb n n][c nb NBIG][misc nb kMisc][mu nb itv][V grid LMAX NBIG][act nb NBIG]
+static size_t filter_big_workspace_bytes(int n, int64_t d, int itv) {
+  const int64_t nchunks = cdiv(d, itv);
+  const int64_t b = nchunks < kBatchBig ? nchunks : kBatchBig;
+  const int64_t grid = b < kBigGrid ? b : kBigGrid;
+  return 256 + static_cast<size_t>(b) * (sizeof(double) * (static_cast<size_t>(n) * n + NBIG + kMisc + itv) +
+                                         sizeof(int) * NBIG) +
+         static_cast<size_t>(grid) * LMAX * NBIG * sizeof(double) + 256;
+}
+
+int launch_filter_big(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
+                      double expansion, double* out, int* status, int* trace, void* ws, hipStream_t s) {
+  const int64_t nchunks = cdiv(d, itv);
+  const int64_t bmax = nchunks < kBatchBig ? nchunks : kBatchBig;
+  const int grid_max = static_cast<int>(bmax < kBigGrid ? bmax : kBigGrid);
+  char* base = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  double* Gws = reinterpret_cast<double*>(base);
+  double* cws = Gws + static_cast<size_t>(bmax) * n * n;
+  double* mws = cws + static_cast<size_t>(bmax) * NBIG;
+  double* muws = mws + static_cast<size_t>(bmax) * kMisc;
+  double* Vws = muws + static_cast<size_t>(bmax) * itv;
+  int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(grid_max) * LMAX * NBIG);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&filter_big_kernel<0>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     static_cast<int>(kBigLds));
+  static const hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&filter_big_kernel<1>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      static_cast<int>(kBigLds));
+  SRA_REQUIRE(attr == hipSuccess && attr1 == hipSuccess, SRA_ERR_UNSUPPORTED,
+              "filter_big_kernel: cannot reserve %zu bytes of LDS", kBigLds);
+  const int nbk = static_cast<int>(cdiv(n, kBigTile));
+  for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
+    const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
+    const int64_t jend = (c0 + nb) * static_cast<int64_t>(itv);
+    const int64_t ncols = (jend < d ? jend : d) - c0 * static_cast<int64_t>(itv);
+    hipLaunchKernelGGL(chunk_colmean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, muws);
+    int rc = launch_status("chunk_colmean_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(chunk_gram_big_kernel, dim3(nbk * (nbk + 1) / 2, nb), dim3(256), 0, s, X, n, d, ldx, itv, c0,
+                       muws, Gws);
+    rc = launch_status("chunk_gram_big_kernel");
+    if (rc) return rc;
+    if (mode == 1) {
+      hipLaunchKernelGGL(noregret_pre_big_kernel, dim3(nb), dim3(kBigThreads), 0, s, Gws, n, eps, aws, mws);
+      rc = launch_status("noregret_pre_big_kernel");
+      if (rc) return rc;
+    }
+    BigArgs ba{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, Vws,
+               trace != nullptr ? trace + static_cast<size_t>(c0) * (1 + 2 * n) : nullptr};
+    const int grid = nb < grid_max ? nb : grid_max;
+    if (mode == 0) hipLaunchKernelGGL(filter_big_kernel<0>, dim3(grid), dim3(kBigThreads), kBigLds, s, ba);
+    else hipLaunchKernelGGL(filter_big_kernel<1>, dim3(grid), dim3(kBigThreads), kBigLds, s, ba);
+    rc = launch_status("filter_big_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws, aws,
+                       mws, out, NBIG);
+    rc = launch_status("chunk_mean_kernel");
+    if (rc) return rc;
+  }
+  return SRA_OK;
+}
+
+size_t filter_workspace_bytes(int n, int64_t d, int itv) {
+  if (n > FNP) return filter_big_workspace_bytes(n, d, itv);
   const int64_t nchunks = cdiv(d, itv);
   const int64_t b = nchunks < kBatch ? nchunks : kBatch;
   const int64_t grid = b < kLanczosGrid ? b : kLanczosGrid;
@@ -2069,12 +2664,16 @@ size_t filter_workspace_bytes(int64_t d, int itv) {
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
                   double expansion, double* out, int* status, double* dbg, int* trace, void* ws, size_t ws_bytes,
                   hipStream_t s) {
-  SRA_REQUIRE(n >= 1 && n <= FNP, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", FNP, n);
+  SRA_REQUIRE(n >= 1 && n <= NBIG, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", NBIG, n);
   SRA_REQUIRE(itv >= 1, SRA_ERR_ARG, "itv must be >= 1");
   const int64_t nchunks = cdiv(d, itv);
   SRA_REQUIRE(nchunks < (int64_t(1) << 31), SRA_ERR_ARG, "too many chunks");
-  SRA_REQUIRE(ws != nullptr && ws_bytes >= filter_workspace_bytes(d, itv), SRA_ERR_WORKSPACE,
-              "filter workspace too small: need %zu bytes", filter_workspace_bytes(d, itv));
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= filter_workspace_bytes(n, d, itv), SRA_ERR_WORKSPACE,
+              "filter workspace too small: need %zu bytes", filter_workspace_bytes(n, d, itv));
+  if (n > FNP) {
+    SRA_REQUIRE(dbg == nullptr, SRA_ERR_UNSUPPORTED, "filter debug records support N <= %d (got %d)", FNP, n);
+    return launch_filter_big(mode, X, n, d, ldx, itv, eps, sigma, expansion, out, status, trace, ws, s);
+  }
   const int64_t bmax = nchunks < kBatch ? nchunks : kBatch;
   const int lgrid_max = static_cast<int>(bmax < kLanczosGrid ? bmax : kLanczosGrid);
   char* base = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
@@ -2141,7 +2740,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     const int64_t jend = (c0 + nb) * static_cast<int64_t>(itv);
     const int64_t ncols = (jend < d ? jend : d) - c0 * static_cast<int64_t>(itv);
     hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws,
-                       aws, mws, out);
+                       aws, mws, out, FNP);
     rc = launch_status("chunk_mean_kernel");
     if (rc) return rc;
   }
@@ -2169,7 +2768,7 @@ static int filter_checks(const float* X, int64_t n, int64_t d, int64_t ldx, int3
 extern "C" int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
   SRA_REQUIRE(n >= 1 && d >= 1 && itv >= 1, SRA_ERR_SHAPE, "bad shape");
-  *bytes = sra::filter_workspace_bytes(d, itv);
+  *bytes = sra::filter_workspace_bytes(static_cast<int>(n), d, itv);
   return SRA_OK;
 }
 

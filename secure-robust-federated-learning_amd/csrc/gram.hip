@@ -121,8 +121,14 @@ __device__ __forceinline__ float sum_lanes_16_32(float x) {
   return x;
 }
 
+// Row r of the (virtual) input is X + r ldx for r < split, else X2 + (r - split)
+// ldx: two 128-row blocks of a larger matrix side by side (N > 256, the pair
+// path below).  shift != nullptr replaces the per-stage client mean by a
+// fixed per-coordinate shift (the mean over ALL N clients), so the pairs'
+// Grams are centred alike and assemble into one matrix.
 template <int NB, int WAVES, bool VEC, int TG>
-__device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, int64_t d, int64_t ldx, int64_t chunk,
+__device__ __forceinline__ void gram_body(const float* __restrict__ X, const float* __restrict__ X2, int split, int n,
+                                          int64_t d, int64_t ldx, const float* __restrict__ shift, int64_t chunk,
                                           float* __restrict__ slab, float* lds) {
   using C = GramCfg<NB, WAVES>;
   constexpr int STAGE = C::STAGE;
@@ -164,7 +170,8 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
       const int row = row0 + C::RSTEP * q;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (row < n && row < C::NP) {
-        const float* p = X + static_cast<int64_t>(row) * ldx + k0;
+        const float* p = (row < split ? X + static_cast<int64_t>(row) * ldx
+                                      : X2 + static_cast<int64_t>(row - split) * ldx) + k0;
         if (VEC && k0 + 3 < k_end) {
           v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
         } else {
@@ -200,7 +207,12 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
   };
 
   // column means of a stored stage: fixed order over the waves' partials
-  auto stage_means = [&](float* mu) {
+  auto stage_means = [&](float* mu, int s) {
+    if (shift != nullptr) {
+      const int64_t c0 = (static_cast<int64_t>(s) * gridDim.x + blockIdx.x) * STAGE;
+      for (int c = tid; c < STAGE; c += C::THREADS) mu[c] = c0 + c < k_end ? shift[c0 + c] : 0.f;
+      return;
+    }
     for (int c = tid; c < STAGE; c += C::THREADS) {
       float m = part[c];
 #pragma unroll
@@ -214,7 +226,7 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
     store_stage(bufp(0), part);
     if (nstage > 1) load_stage(1);
     __syncthreads();
-    stage_means(mup(0));
+    stage_means(mup(0), 0);
     __syncthreads();
   }
 
@@ -265,7 +277,7 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
     }
     __syncthreads();
     if (s + 1 < nstage) {
-      stage_means(mup((s + 1) & 1));
+      stage_means(mup((s + 1) & 1), s + 1);
       __syncthreads();
     }
   }
@@ -287,24 +299,28 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, int n, in
 }
 
 template <int NB, int WAVES, bool VEC>
-__global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* __restrict__ X, int n, int64_t d,
-                                                                  int64_t ldx, int64_t chunk,
+__global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* __restrict__ X,
+                                                                  const float* __restrict__ X2, int split, int n,
+                                                                  int64_t d, int64_t ldx,
+                                                                  const float* __restrict__ shift, int64_t chunk,
                                                                   float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int WT = GramCfg<NB, WAVES>::WT;
   const int tg = (threadIdx.x >> 6) % WT;  // wave-uniform
-  if (tg == 0) gram_body<NB, WAVES, VEC, 0>(X, n, d, ldx, chunk, slab, lds);
-  if constexpr (WT > 1) if (tg == 1) gram_body<NB, WAVES, VEC, 1>(X, n, d, ldx, chunk, slab, lds);
+#define SRA_GB(TGV) gram_body<NB, WAVES, VEC, TGV>(X, X2, split, n, d, ldx, shift, chunk, slab, lds)
+  if (tg == 0) SRA_GB(0);
+  if constexpr (WT > 1) if (tg == 1) SRA_GB(1);
   if constexpr (WT > 2) {
-    if (tg == 2) gram_body<NB, WAVES, VEC, 2>(X, n, d, ldx, chunk, slab, lds);
-    if (tg == 3) gram_body<NB, WAVES, VEC, 3>(X, n, d, ldx, chunk, slab, lds);
+    if (tg == 2) SRA_GB(2);
+    if (tg == 3) SRA_GB(3);
   }
   if constexpr (WT > 4) {
-    if (tg == 4) gram_body<NB, WAVES, VEC, 4>(X, n, d, ldx, chunk, slab, lds);
-    if (tg == 5) gram_body<NB, WAVES, VEC, 5>(X, n, d, ldx, chunk, slab, lds);
-    if (tg == 6) gram_body<NB, WAVES, VEC, 6>(X, n, d, ldx, chunk, slab, lds);
-    if (tg == 7) gram_body<NB, WAVES, VEC, 7>(X, n, d, ldx, chunk, slab, lds);
+    if (tg == 4) SRA_GB(4);
+    if (tg == 5) SRA_GB(5);
+    if (tg == 6) SRA_GB(6);
+    if (tg == 7) SRA_GB(7);
   }
+#undef SRA_GB
 }
 
 // Slab reduction in a fixed order (deterministic), fp64, two levels:
@@ -352,6 +368,42 @@ __global__ void __launch_bounds__(256) gram_reduce2_kernel(const double* __restr
   G[static_cast<int64_t>(j) * n + i] = s;
 }
 
+// Pair path (N > 256): the entries of a virtual pair matrix [block a; block b]
+// land at rows off_a + i (i < split) / off_b + i - split of the N x N G; the
+// diagonal blocks only where asked (each entry of G is written by one pair).
+template <int NB>
+__global__ void __launch_bounds__(256) gram_reduce2_pair_kernel(const double* __restrict__ partial, int n, int split,
+                                                                int off_a, int off_b, int ldg, int write_aa,
+                                                                int write_bb, double* __restrict__ G) {
+  using C = GramCfg<NB>;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= C::T * 1024) return;
+  const int tile = e >> 10;
+  const int el = e & 1023;
+  const int i = 32 * C::kTileI(tile) + (el >> 5);
+  const int j = 32 * C::kTileJ(tile) + (el & 31);
+  if (i >= n || j >= n) return;
+  const bool ia = i < split, ja = j < split;
+  if ((ia && ja && !write_aa) || (!ia && !ja && !write_bb)) return;
+  double s = 0.0;
+#pragma unroll 8
+  for (int g = 0; g < kRedGroups; ++g) s += partial[static_cast<int64_t>(g) * C::T * 1024 + e];
+  const int64_t gi = ia ? off_a + i : off_b + i - split;
+  const int64_t gj = ja ? off_a + j : off_b + j - split;
+  G[gi * ldg + gj] = s;
+  G[gj * ldg + gi] = s;
+}
+
+// fp32 column mean over the n rows (sequential, like the stage means)
+__global__ void __launch_bounds__(256) gram_shift_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                                         float* __restrict__ shift) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= d) return;
+  float m = 0.f;
+  for (int i = 0; i < n; ++i) m += X[static_cast<int64_t>(i) * ldx + j];
+  shift[j] = m * (1.0f / static_cast<float>(n));
+}
+
 int gram_num_wg(int64_t d) {
   const int64_t stages = cdiv(d, 64);
   return static_cast<int>(stages < 256 ? (stages > 0 ? stages : 1) : 256);
@@ -371,23 +423,36 @@ static int gram_waves(int nb) {
   return nb <= 4 ? 4 : 8;
 }
 
+// pair: (off_a, off_b, split, ldg, write_aa, write_bb) of the pair path, or
+// nullptr for a whole matrix of n <= 256 rows
+struct GramPair {
+  const float* X2;
+  const float* shift;
+  int split, off_a, off_b, ldg, write_aa, write_bb;
+};
+
 template <int NB, int WAVES>
-static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s) {
+static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s,
+                           const GramPair* pr = nullptr) {
   using C = GramCfg<NB, WAVES>;
   const int nwg = gram_num_wg(d);
   const int64_t chunk = cdiv(cdiv(d, nwg), C::STAGE) * C::STAGE;
   const size_t lds = sizeof(float) * C::lds_floats;
-  const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  const float* X2 = pr ? pr->X2 : X;
+  const int split = pr ? pr->split : n;
+  const float* shift = pr ? pr->shift : nullptr;
+  const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(X2) & 15) == 0);
   if (vec) {
     SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true>), dim3(nwg), dim3(C::THREADS), lds, s, X, n, d, ldx,
-                       chunk, slab);
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split, n,
+                       d, ldx, shift, chunk, slab);
   } else {
     SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false>), dim3(nwg), dim3(C::THREADS), lds, s, X, n, d, ldx,
-                       chunk, slab);
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split, n,
+                       d, ldx, shift, chunk, slab);
   }
   int rc = launch_status("gram_partial_kernel");
   if (rc) return rc;
@@ -396,30 +461,69 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
                      static_cast<int64_t>(nwg) * C::WK, partial);
   rc = launch_status("gram_reduce1_kernel");
   if (rc) return rc;
+  if (pr) {
+    hipLaunchKernelGGL((gram_reduce2_pair_kernel<NB>), dim3(cdiv(C::T * 1024, 256)), dim3(256), 0, s, partial, n,
+                       pr->split, pr->off_a, pr->off_b, pr->ldg, pr->write_aa, pr->write_bb, G);
+    return launch_status("gram_reduce2_pair_kernel");
+  }
   hipLaunchKernelGGL((gram_reduce2_kernel<NB>), dim3(cdiv(C::T * 1024, 256)), dim3(256), 0, s, partial, n, G);
   return launch_status("gram_reduce2_kernel");
 }
 
 template <int NB>
-static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s) {
-  if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s);
-  return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s);
+static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s,
+                          const GramPair* pr = nullptr) {
+  if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
+  return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s, pr);
 }
 
+constexpr int kGramMaxClients = 512;
+constexpr int kGramPairRows = 128;
+
 size_t gram_workspace_bytes(int n, int64_t d) {
-  // sized for the larger of the 4- and 8-wave slab layouts (WK <= 8)
-  const int nb = static_cast<int>(cdiv(n, 32));
+  // sized for the larger of the 4- and 8-wave slab layouts (WK <= 8); N > 256:
+  // the 256-row pair layout plus the d-vector shift
+  const int nb = static_cast<int>(cdiv(n > 256 ? 256 : n, 32));
   const int T = nb * (nb + 1) / 2;
-  return sizeof(float) * static_cast<size_t>(gram_num_wg(d)) * 8 * T * 1024 +
-         sizeof(double) * static_cast<size_t>(kRedGroups) * T * 1024;
+  const size_t base = sizeof(float) * static_cast<size_t>(gram_num_wg(d)) * 8 * T * 1024 +
+                      sizeof(double) * static_cast<size_t>(kRedGroups) * T * 1024;
+  return n > 256 ? base + 256 + sizeof(float) * static_cast<size_t>(d) : base;
+}
+
+// N in (256, kGramMaxClients]: clients in blocks of 128; one 256-row launch per
+// pair of blocks (p, q), p < q, all centred by the same shift (the fp32 mean
+// over all N clients) and run in the same configuration (NB = 8), so every
+// entry is accumulated alike whichever pair produced it (identical clients
+// still get G_ii == G_jj == G_ij).  Cross blocks come from their pair, the
+// diagonal block p from (p, p + 1), the last one from the last pair.
+static int launch_gram_pairs(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s) {
+  const int nblk = static_cast<int>(cdiv(n, kGramPairRows));
+  const size_t base = gram_workspace_bytes(256, d);
+  float* shift = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(slab) + base + 255) & ~uintptr_t(255));
+  hipLaunchKernelGGL(gram_shift_kernel, dim3(cdiv(d, 256)), dim3(256), 0, s, X, n, d, ldx, shift);
+  int rc = launch_status("gram_shift_kernel");
+  if (rc) return rc;
+  for (int p = 0; p < nblk; ++p) {
+    for (int q = p + 1; q < nblk; ++q) {
+      const int rows_q = q == nblk - 1 ? n - q * kGramPairRows : kGramPairRows;
+      GramPair pr{X + static_cast<int64_t>(q) * kGramPairRows * ldx, shift, kGramPairRows, p * kGramPairRows,
+                  q * kGramPairRows, n, q == p + 1 ? 1 : 0, (p == nblk - 2 && q == nblk - 1) ? 1 : 0};
+      rc = launch_gram_nb<8>(X + static_cast<int64_t>(p) * kGramPairRows * ldx, kGramPairRows + rows_q, d, ldx, G,
+                             slab, s, &pr);
+      if (rc) return rc;
+    }
+  }
+  return SRA_OK;
 }
 
 int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes,
                 hipStream_t s) {
-  SRA_REQUIRE(n >= 1 && n <= 256, SRA_ERR_UNSUPPORTED, "Gram supports 1 <= N <= 256 (got %d)", n);
+  SRA_REQUIRE(n >= 1 && n <= kGramMaxClients, SRA_ERR_UNSUPPORTED, "Gram supports 1 <= N <= %d (got %d)",
+              kGramMaxClients, n);
   SRA_REQUIRE(ws != nullptr && ws_bytes >= gram_workspace_bytes(n, d), SRA_ERR_WORKSPACE,
               "Gram workspace too small: need %zu bytes", gram_workspace_bytes(n, d));
   float* slab = static_cast<float*>(ws);
+  if (n > 256) return launch_gram_pairs(X, n, d, ldx, G, slab, s);
   switch (cdiv(n, 32)) {
     case 1: return launch_gram_nb<1>(X, n, d, ldx, G, slab, s);
     case 2: return launch_gram_nb<2>(X, n, d, ldx, G, slab, s);
@@ -436,7 +540,8 @@ int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* 
 
 extern "C" int sra_gram_workspace_bytes(int64_t n, int64_t d, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
-  SRA_REQUIRE(n >= 1 && n <= 256 && d >= 1, SRA_ERR_UNSUPPORTED, "Gram supports 1 <= N <= 256, d >= 1");
+  SRA_REQUIRE(n >= 1 && n <= sra::kGramMaxClients && d >= 1, SRA_ERR_UNSUPPORTED, "Gram supports 1 <= N <= %d, d >= 1",
+              sra::kGramMaxClients);
   *bytes = sra::gram_workspace_bytes(static_cast<int>(n), d);
   return SRA_OK;
 }

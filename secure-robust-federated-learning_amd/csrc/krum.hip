@@ -19,7 +19,7 @@
 
 namespace sra {
 
-constexpr int kMaxClients = 256;
+constexpr int kMaxClients = 512;
 
 // numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src) for
 // float32, n elements at a[0..n): < 8 sequential from 0; <= 128 eight
@@ -137,12 +137,18 @@ __device__ __forceinline__ float wave_pw_block_f32(const float* a, int n) {
   return res;
 }
 
-// np_pairwise_f32 over one wave (n <= 256: at most one split)
+// np_pairwise_f32 over one wave (n <= 512: at most two levels of splits)
 __device__ __forceinline__ float wave_pairwise_f32(const float* a, int n) {
   if (n <= 128) return wave_pw_block_f32(a, n);
+  auto half = [&](const float* b, int m) -> float {
+    if (m <= 128) return wave_pw_block_f32(b, m);
+    int q = m / 2;
+    q -= q % 8;
+    return wave_pw_block_f32(b, q) + wave_pw_block_f32(b + q, m - q);
+  };
   int n2 = n / 2;
   n2 -= n2 % 8;
-  return wave_pw_block_f32(a, n2) + wave_pw_block_f32(a + n2, n - n2);
+  return half(a, n2) + half(a + n2, n - n2);
 }
 
 // `rounds` Krum selections over a shrinking alive set (rounds = 1: plain krum).
@@ -155,22 +161,24 @@ __device__ __forceinline__ float wave_pairwise_f32(const float* a, int n) {
 // tail), then a wave-parallel first minimum.  (Round 1 summed on one lane per
 // row from global memory: 2.5 ms for Bulyan's 88 rounds at N = 128.)
 constexpr int kKrumGStaged = 128;   // compacted-row stride (m <= 125 for N <= 128)
-constexpr int kKrumGGlobal = 256;
+constexpr int kKrumGGlobal = 256;   // N <= 258 (m <= 256), eight rows per wave batch
+constexpr int kKrumGBig = 512;      // N <= kMaxClients, two rows per wave batch (LDS)
 
-template <bool STAGED>
+// U: rows compacted per wave batch (eight, or two for the 512-wide rows)
+template <bool STAGED, int GS = STAGED ? kKrumGStaged : kKrumGGlobal, int U = 8>
 __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restrict__ Sg, const int* __restrict__ Jg,
                                                            int n, int f, int rounds, int* __restrict__ order,
                                                            float* __restrict__ scores0, int* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) char kr_smem[];
-  constexpr int GS = STAGED ? kKrumGStaged : kKrumGGlobal;
+  static_assert(U == 8 || !STAGED, "the staged kernel compacts eight rows per batch");
   __shared__ unsigned char alive[kMaxClients];
   __shared__ float score[kMaxClients];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int nwaves = blockDim.x >> 6;
-  float* gath = reinterpret_cast<float*>(kr_smem);                            // [16][8][GS]
-  float* Ss = gath + 16 * 8 * GS;                                            // [n][n] when staged
+  float* gath = reinterpret_cast<float*>(kr_smem);                            // [16][U][GS]
+  float* Ss = gath + 16 * U * GS;                                            // [n][n] when staged
   unsigned char* Js = reinterpret_cast<unsigned char*>(Ss + (STAGED ? n * n : 0));
   if constexpr (STAGED) {
     for (int e = tid; e < n * n; e += blockDim.x) {
@@ -180,15 +188,15 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
   }
   for (int i = tid; i < n; i += blockDim.x) alive[i] = 1;
   __syncthreads();
-  float* gw = gath + wave * 8 * GS;
+  float* gw = gath + wave * U * GS;
   const int u_me = lane >> 3, k_me = lane & 7;
   for (int t = 0; t < rounds; ++t) {
     const int nr = n - t;
     const int m = slice_count(nr - f - 2, nr - 1);
-    for (int u0 = 0; wave + nwaves * u0 < n; u0 += 8) {
-      // compaction of up to eight rows
+    for (int u0 = 0; wave + nwaves * u0 < n; u0 += U) {
+      // compaction of up to U rows
 #pragma unroll 1
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int i = wave + nwaves * (u0 + u);
         if (i >= n || !alive[i]) continue;   // wave-uniform
         int c = 0;
@@ -207,8 +215,8 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
       __builtin_amdgcn_wave_barrier();
       // numpy pairwise sums of the eight compacted rows
       const int i_me = wave + nwaves * (u0 + u_me);
-      const bool row_ok = i_me < n && alive[i_me];
-      const float* a = gw + u_me * GS;
+      const bool row_ok = u_me < U && i_me < n && alive[i_me];
+      const float* a = gw + (u_me < U ? u_me : 0) * GS;
       float sc = 0.f;
       if (m <= 128) {
         const int n8 = m - (m % 8);
@@ -232,7 +240,7 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
       } else {
         // N > 130: one row at a time over the whole wave (numpy's split at n/2)
 #pragma unroll 1
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int i = wave + nwaves * (u0 + u);
           if (i >= n || !alive[i]) continue;
           const float v = wave_pairwise_f32(gw + u * GS, m);
@@ -328,10 +336,23 @@ int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int*
       return launch_status("krum_rounds_kernel");
     }
   }
+  if (n > kKrumGGlobal + 2) {   // compacted rows longer than 256
+    constexpr int lds_big = 16 * 2 * kKrumGBig * 4;
+    static const hipError_t attr_b =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(krum_rounds_kernel<false, kKrumGBig, 2>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds_big);
+    SRA_REQUIRE(attr_b == hipSuccess, SRA_ERR_UNSUPPORTED,
+                "krum_rounds_kernel: cannot reserve %d bytes of dynamic LDS (%s)", lds_big, hipGetErrorString(attr_b));
+    hipLaunchKernelGGL((krum_rounds_kernel<false, kKrumGBig, 2>), dim3(1), dim3(1024), lds_big, s, S, J, n, f, rounds,
+                       order, scores0, nullptr);
+    return launch_status("krum_rounds_kernel");
+  }
   static const hipError_t attr_g =
       hipFuncSetAttribute(reinterpret_cast<const void*>(krum_rounds_kernel<false>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 8 * kKrumGGlobal * 4);
-  (void)attr_g;
+  SRA_REQUIRE(attr_g == hipSuccess, SRA_ERR_UNSUPPORTED,
+              "krum_rounds_kernel: cannot reserve %d bytes of dynamic LDS (%s)", 16 * 8 * kKrumGGlobal * 4,
+              hipGetErrorString(attr_g));
   hipLaunchKernelGGL(krum_rounds_kernel<false>, dim3(1), dim3(1024), 16 * 8 * kKrumGGlobal * 4, s, S, J, n, f, rounds,
                      order, scores0, nullptr);
   return launch_status("krum_rounds_kernel");

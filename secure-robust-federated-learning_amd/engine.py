@@ -250,9 +250,12 @@ def chunk_width(d, itv):
     return int(itv)
 
 
-def _filter(X, mode, eps, sigma, expansion, itv, check):
+def _filter(X, mode, eps, sigma, expansion, itv, check, out=None):
     X, n, d, ldx = as_matrix(X)
-    out = torch.empty(d, dtype=torch.float64, device=X.device)
+    if out is None:
+        out = torch.empty(d, dtype=torch.float64, device=X.device)
+    elif out.dtype != torch.float64 or out.numel() != d or not out.is_contiguous() or out.device != X.device:
+        raise ValueError("out must be a contiguous float64 (d,) tensor on X's device")
     status = torch.zeros(1, dtype=torch.int32, device=X.device)
     w = chunk_width(d, itv)
     nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
@@ -277,14 +280,15 @@ def filter_trace(X, mode, eps, sigma, expansion, itv):
     status = torch.zeros(1, dtype=torch.int32, device=X.device)
     w = chunk_width(d, itv)
     nch = -(-d // w)
-    tr = torch.full((nch, FILTER_TRACE_STRIDE), -1, dtype=torch.int32, device=X.device)
+    half = max(n, 128)   # rows of 1 + 2 max(N, 128) int32 (include/sra.h)
+    tr = torch.full((nch, 1 + 2 * half), -1, dtype=torch.int32, device=X.device)
     nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
     ws = _workspace(nb, X.device)
     _lib.call("sra_filter_trace_f32", X.data_ptr(), n, d, ldx, int(mode), w, float(eps), float(sigma),
               float(expansion), out.data_ptr(), status.data_ptr(), tr.data_ptr(), ws.data_ptr(), nb,
               _stream_ptr(X.device))
     tr = tr.cpu().numpy()
-    return out, np.concatenate([tr[:, :1 + n], tr[:, 1 + 128:1 + 128 + n]], axis=1)
+    return out, np.concatenate([tr[:, :1 + n], tr[:, 1 + half:1 + half + n]], axis=1)
 
 
 FILTER_DEBUG_DOUBLES = 128 * 128 + 256 * 144
@@ -311,14 +315,14 @@ def filter_debug(X, mode, eps, sigma, expansion, itv):
     return out, G, recs
 
 
-def filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, check=True):
-    """robust_estimator.filterL2 on device: float64 (d,)."""
-    return _filter(X, 0, eps, sigma, expansion, itv, check)
+def filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, check=True, out=None):
+    """robust_estimator.filterL2 on device: float64 (d,) (into ``out`` when given)."""
+    return _filter(X, 0, eps, sigma, expansion, itv, check, out)
 
 
-def ex_noregret(X, eps=1. / 12, sigma=1, expansion=20, itv=ITV, check=True):
-    """robust_estimator.ex_noregret on device: float64 (d,)."""
-    return _filter(X, 1, eps, sigma, expansion, itv, check)
+def ex_noregret(X, eps=1. / 12, sigma=1, expansion=20, itv=ITV, check=True, out=None):
+    """robust_estimator.ex_noregret on device: float64 (d,) (into ``out`` when given)."""
+    return _filter(X, 1, eps, sigma, expansion, itv, check, out)
 
 
 def mom_bucket_count(n, eps, delta):
@@ -331,16 +335,18 @@ def mom_bucket_count(n, eps, delta):
     return num, size
 
 
-def mom_filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True):
+def mom_filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True,
+                  out=None):
     n = int(X.shape[0])
     num, size = mom_bucket_count(n, eps, delta)
-    return filter_l2(bucket_means(X, size, num), eps, sigma, expansion, itv, check)
+    return filter_l2(bucket_means(X, size, num), eps, sigma, expansion, itv, check, out)
 
 
-def mom_ex_noregret(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True):
+def mom_ex_noregret(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True,
+                    out=None):
     n = int(X.shape[0])
     num, size = mom_bucket_count(n, eps, delta)
-    return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check)
+    return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check, out)
 
 
 # ---------------------------------------------------------------------------

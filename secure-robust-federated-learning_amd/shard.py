@@ -106,7 +106,8 @@ def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
     assembles the (d,) float64 result.
 
     ops: bulyan_round(X, rows, nr, aggsubfunc, agg_out) -> dist (nr,) float64;
-         bulyan_pick(dist, rows, nr, rows_next); bulyan_stage(S, beta) -> (w,);
+         bulyan_pick(dist, rows, nr, rows_next, status) (status[0] = 1 when no
+         distance is finite); bulyan_stage(S, beta) -> (w,);
          gram(X) -> (N, N) float64; krum_rounds(G, f, rounds) -> (rounds,) indices."""
     n = int(X_shard.shape[0])
     theta = n - 2 * int(f)
@@ -127,13 +128,20 @@ def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
         S = torch.empty((theta, X_shard.shape[1]), dtype=torch.float32, device=X_shard.device)
         rows = torch.arange(n, dtype=torch.int32, device=X_shard.device)
         nxt = torch.empty_like(rows)
+        # set to 1 by a pick that finds no finite minimum (every distance NaN /
+        # inf); checked once after the rounds (one host sync)
+        status = torch.zeros(1, dtype=torch.int32, device=X_shard.device)
         for t in range(theta):
             nr = n - t
             dvec = ops["bulyan_round"](X_shard, rows, nr, aggsubfunc, S[t])
             if on:
                 dist.all_reduce(dvec, op=dist.ReduceOp.SUM, group=group)
-            ops["bulyan_pick"](dvec, rows, nr, nxt)
+            ops["bulyan_pick"](dvec, rows, nr, nxt, status)
             rows, nxt = nxt, rows
+        if int(status.item()) != 0:
+            # robust_estimator.py:318: `assert selected_idx >= 0` when no
+            # distance is finite (a NaN / inf client in every round's reach)
+            raise AssertionError("bulyan: no finite distance in a selection round (non-finite client update)")
     return gather_columns(ops["bulyan_stage"](S, beta), d, align, group)
 
 
@@ -231,7 +239,7 @@ def engine_ops():
 
     return {
         "bulyan_round": bulyan_round,
-        "bulyan_pick": lambda dvec, rows, nr, nxt: engine.bulyan_pick(dvec, rows, nr, nxt),
+        "bulyan_pick": lambda dvec, rows, nr, nxt, status=None: engine.bulyan_pick(dvec, rows, nr, nxt, status),
         "bulyan_stage": lambda S, beta: engine.bulyan_stage(S, beta),
         "krum_rounds": krum_rounds,
         "average": lambda X: engine.average(X),

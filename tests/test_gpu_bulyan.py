@@ -148,3 +148,41 @@ def test_scalar_helpers_match_reference():
         np.testing.assert_allclose(got, want, rtol=1e-15, atol=0)
         if not orc.bulyan_boundary_tie(a, beta):
             np.testing.assert_allclose(got, z["one"][c], rtol=1e-15, atol=0)
+
+
+@pytest.mark.parametrize("mode", ["median", "trimmedmean"])
+@pytest.mark.parametrize("n,f", [(129, 20), (200, 20), (256, 30), (512, 20)])
+def test_bulyan_many_clients(mode, n, f):
+    """More than 128 clients (the reference has no limit): rounds with more
+    than 128 remaining clients take the LDS k-select + distance passes, the
+    later ones the fused register pass; theta > 128 takes the LDS stage."""
+    d = 400 if n <= 256 else 200
+    x = make_rows(n, d, seed=91 + n + f, byz=f)
+    want, _ = _leftfirst_and_ties(list(x), f, mode)
+    got = engine.bulyan(torch.from_numpy(x).cuda(), f, mode).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("theta,beta", [(160, 80), (129, 1), (300, -40), (472, 392), (511, 100)])
+def test_stage_f32_many_rows(theta, beta):
+    """The per-coordinate stage for theta > 128 (LDS sort, the same exact-span
+    window path, the stage by definition for NaN / inf / wide columns)."""
+    rng = np.random.default_rng(theta + 3 * beta)
+    d = 260
+    S = (0.01 * rng.standard_normal((theta, d))).astype(np.float32)
+    S[:, 60:100] = rng.integers(-3, 4, size=(theta, 40)).astype(np.float32)
+    for c in range(100, 140):
+        r = rng.choice(theta, 2, replace=False)
+        S[r[0], c] *= 1e-12
+        S[r[1], c] *= 1e-30
+    S[rng.integers(0, theta), 140] = np.nan
+    S[rng.integers(0, theta), 141] = np.inf
+    S[rng.integers(0, theta), 142] = -np.inf
+    S[:2, 143] = np.inf
+    S[:, 144] = 0.0
+    got = engine.bulyan_stage(torch.from_numpy(S).cuda(), beta).cpu().numpy()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j].astype(np.float64), beta) for j in range(d)])
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15, equal_nan=True)

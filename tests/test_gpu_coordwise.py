@@ -109,10 +109,11 @@ def test_full_size_properties():
 
 @pytest.mark.parametrize("n", [100, 128])
 @pytest.mark.parametrize("d,ldx", [(64, 64), (65, 68), (1031, 1040), (300_000, 300_000), (299_999, 300_004)])
-def test_lds_dma_path_bitexact(n, d, ldx):
-    """The persistent LDS-DMA k-select (exact N = 100 / 128; several tiles per
-    wave, a partial last tile served by the register path, padded rows) with
-    NaN / inf columns, against the oracle."""
+def test_exact_n_paths_ragged_bitexact(n, d, ldx):
+    """The exact-N k-select paths (select_plain_kernel for the trimmed mean,
+    select_reg_kernel for the median; N = 100 / 128) over ragged widths (a
+    partial last 64-coordinate tile) and padded rows (ldx > d), with NaN / inf
+    columns, against the oracle."""
     import warnings
     rng = np.random.default_rng(n + d)
     full = make_rows(n, ldx, seed=d + n)

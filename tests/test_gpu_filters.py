@@ -219,3 +219,46 @@ def test_c5_mom_filterl2_per_gpu_shard_chunks():
     assert np.isfinite(got).all()
     _chunk_check(B, got, [0, 12499],
                  lambda xs, o, pt, tr: orc.filterL2(xs, order=o, perturb=pt, trace=tr, **SIM), 0, gtrace=gtr)
+
+
+@pytest.mark.parametrize("n,k,itv,eps", [(129, 300, 150, 0.03), (200, 300, 150, 0.02), (256, 256, 256, 0.02),
+                                         (512, 300, 300, 0.01)])
+def test_filterl2_many_clients(n, k, itv, eps):
+    """N > 128 (the reference has no client limit): the big-N path (global
+    Gram blocks, the 1024-thread re-orthogonalising solver) against the
+    oracle over a few iterations (sigma 1e-5: no early exit), including
+    N > itv (client space larger than the chunk)."""
+    x = make_rows(n, k, seed=700 + n, byz=max(1, n // 6))
+    want = orc.filterL2(list(x), eps, 1e-5, 20, itv)
+    got = engine.filter_l2(torch.from_numpy(x).cuda(), eps, 1e-5, 20, itv).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("n,k,itv,eps", [(129, 200, 100, 0.05), (200, 200, 200, 0.03), (256, 150, 150, 0.03),
+                                         (512, 128, 128, 0.01)])
+def test_ex_noregret_many_clients(n, k, itv, eps):
+    x = make_rows(n, k, seed=800 + n, byz=max(1, n // 6))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want = orc.ex_noregret(list(x), eps, 1e-5, 20, itv)
+    got = engine.ex_noregret(torch.from_numpy(x).cuda(), eps, 1e-5, 20, itv).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("mode,n,k,eps", [(0, 200, 400, 0.1), (0, 512, 300, 0.05), (1, 256, 300, 0.05)])
+def test_many_clients_decision_trace(mode, n, k, eps):
+    """Long runs at N > 128 (sigma 1e-5): the device's per-iteration decisions
+    (removed client / capped count, the final active set) equal the
+    client-space oracle's on the prefix where two client orders and four
+    1e-13 weight nudges all agree (oracle.robust_np.trace_pair)."""
+    x = make_rows(n, k, seed=900 + n + mode, byz=max(1, n // 6))
+    out, tr = engine.filter_trace(torch.from_numpy(x).cuda(), mode, eps, 1e-5, 20, k)
+    a, agree, _ = orc.trace_pair((x, mode, eps, 1e-5, 20))
+    got = tr[0]
+    print("N=%d mode %d: agreed prefix %d of %d iterations" % (n, mode, agree, a[0]))
+    assert agree >= min(10, a[0])
+    np.testing.assert_array_equal(got[1:1 + agree], a[1:1 + agree])
+    if agree == a[0]:
+        assert got[0] == a[0]
+        np.testing.assert_array_equal(got[1 + n:], a[1 + n:])
+    assert np.isfinite(out.cpu().numpy()).all()

@@ -51,7 +51,7 @@ def test_golden_mom_krum(rec):
     np.testing.assert_array_equal(got, rec["out"])
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 31, 32, 33, 64, 100, 128, 129, 160, 200, 256])
+@pytest.mark.parametrize("n", [1, 2, 3, 31, 32, 33, 64, 100, 128, 129, 160, 200, 256, 257, 300, 384, 512])
 def test_gram_matches_fp64(n):
     d = 3000
     x = make_rows(n, d, seed=200 + n, byz=min(3, n // 4))
@@ -72,9 +72,10 @@ def test_identical_rows_zero_distance_and_unaligned():
             assert G[i, i] + G[j, j] - 2 * G[i, j] == 0.0
 
 
-@pytest.mark.parametrize("n,f", [(128, 20), (100, 20), (64, 10), (20, 25)])
+@pytest.mark.parametrize("n,f", [(128, 20), (100, 20), (64, 10), (20, 25), (129, 20), (200, 20), (256, 40),
+                                 (300, 20), (512, 50)])
 def test_krum_index_against_oracle(n, f):
-    d = 20_000
+    d = 20_000 if n <= 256 else 4_000
     x = make_rows(n, d, seed=300 + n, byz=min(f, n // 3))
     xs = list(x)
     want_scores = orc.krum_(xs, f)
@@ -116,3 +117,27 @@ def test_bucket_means_and_empty_bucket():
     np.testing.assert_array_equal(B, want)
     with pytest.raises(ValueError):
         engine.bucket_means(X, 4, 14)     # bucket 13 would start at row 52 > 50
+
+
+def test_identical_rows_zero_distance_pairs():
+    """N > 256 (the pair path: 128-row blocks, one launch per pair, a common
+    shift): identical clients spread over different blocks still get exactly
+    zero distance."""
+    x = make_rows(400, 3000, seed=6, byz=0)
+    for r in (5, 130, 260, 399):
+        x[r] = x[77]
+    G = engine.gram(torch.from_numpy(x).cuda()).cpu().numpy()
+    same = [77, 5, 130, 260, 399]
+    for i in same:
+        for j in same:
+            assert G[i, i] + G[j, j] - 2 * G[i, j] == 0.0, (i, j)
+
+
+@pytest.mark.parametrize("n,f", [(300, 20), (512, 100)])
+def test_bulyan_krum_many_clients(n, f):
+    """Bulyan-Krum with N > 256: the pair Gram, the 512-wide Krum rounds and
+    (theta > 128) the LDS per-coordinate stage, against the oracle's selection."""
+    x = make_rows(n, 300, seed=n + f, byz=f // 2)
+    _, removed = orc.bulyan_select(list(x), f, "krum")
+    _, sel = engine.bulyan(torch.from_numpy(x).cuda(), f, "krum", selected=True)
+    assert sel.cpu().tolist() == removed

@@ -55,12 +55,14 @@ def cpu_bulyan_ops():
         agg.copy_(torch.from_numpy(a))
         return torch.from_numpy(((sub.astype(np.float64) - a.astype(np.float64)) ** 2).sum(axis=1))
 
-    def bulyan_pick(dvec, rows, nr, nxt):
+    def bulyan_pick(dvec, rows, nr, nxt, status=None):
         dv = dvec.numpy()
         best, bv = -1, np.inf
         for r in range(nr):
             if dv[r] < bv:
                 best, bv = r, dv[r]
+        if best < 0 and status is not None:
+            status[0] = 1
         keep = [rows[r].item() for r in range(nr) if r != max(best, 0)]
         nxt[:nr - 1] = torch.tensor(keep, dtype=torch.int32)
 
@@ -323,3 +325,19 @@ def test_sharded_bulyan_theta_error():
     from srfl_amd import shard
     with pytest.raises(IndexError):
         shard.bulyan(cpu_bulyan_ops(), torch.zeros(10, 4), 4, 5, "median")
+
+
+def test_sharded_bulyan_nonfinite_raises():
+    """A NaN coordinate makes the median-mode round's aggregate NaN in that
+    column, so every distance is NaN and the reference's `assert min_index !=
+    None` (robust_estimator.py:308/321) fires: the sharded path raises the
+    same AssertionError from the pick's status flag."""
+    _setup_paths()
+    import warnings
+    from srfl_amd import shard
+    x = torch.randn(12, 9)
+    x[3, 4] = float("nan")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with pytest.raises(AssertionError):
+            shard.bulyan(cpu_bulyan_ops(), x, 9, 2, "median")
