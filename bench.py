@@ -221,6 +221,32 @@ def solver_flops(agg, X, itv=1000):
     return per_chunk * nchunks, iters
 
 
+BF16_PEAK_TFLOPS = 2500.0     # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def secondary_roofline(agg, n, d, kern_ms):
+    """The other bound of SURVEY.md §8(d) for the same launch: HBM for the
+    MFMA-priced filters (their algorithmic bytes: the chunk Gram pass and the
+    chunk-mean pass each read X once, 4Nd, plus the 8d fp64 output), MFMA for
+    the HBM-priced Krum family (the bf16x3 Gram issues six bf16 32x32x16
+    products per upper 32 x 32 tile and 16-coordinate k-step)."""
+    t = kern_ms * 1e-3
+    if agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
+        nb = n if not agg.startswith("mom_") else engine.mom_bucket_count(n, FILTER_ARGS["eps"], MOM_DELTA)[0]
+        byts = 2 * 4 * nb * d + 8 * d + (4 * n * d + 4 * nb * d if agg.startswith("mom_") else 0)
+        return {"bound": "hbm", "achieved": round(byts / t / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(byts / t / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": byts}
+    if agg in ("krum", "mom_krum", "bulyankrum"):
+        m = n if agg != "mom_krum" else -(-n // 3)
+        nbk = -(-m // 32)
+        flops = 6 * (nbk * (nbk + 1) // 2) * 2 * 32 * 32 * d
+        return {"bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": BF16_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(flops / t / 1e12 / BF16_PEAK_TFLOPS, 4),
+                "issued_bf16_flops_per_launch": flops,
+                "note": "whole op's time; the Gram kernel alone is in profiles/ (kernel stats)"}
+    return None
+
+
 def filter_into(agg):
     """(X_cols, out_view) form of a spectral filter for the pipelined path: the
     block's result is written straight into its slot of the all-gather buffer."""
@@ -460,6 +486,9 @@ def main():
     }
     if solver_note:
         line["roofline"]["model"] = solver_note
+    sec = secondary_roofline(a.agg, n, d, kern_ms)
+    if sec:
+        line["roofline"]["secondary"] = sec
     if rank == 0 and world == 1 and not a.no_host:
         del X
         torch.cuda.empty_cache()

@@ -41,6 +41,7 @@
 //   chunk_mean_kernel   mu_j = sum_i c_i x_ij / sum_i c_i in fp64 over the kept
 //                       clients in client order (the reference's np.average),
 //                       one lane per coordinate; HBM bound.
+#include <cstdlib>
 #include <type_traits>
 
 #include "sra_common.hpp"
@@ -59,7 +60,7 @@ constexpr int TRI = 256;           // per-wave tridiagonal record: alpha[64] bet
 constexpr double kResTol = 1e-16;  // converged when the Ritz residual <= kResTol * lambda
 constexpr double kDgks = 0.5;      // second Gram-Schmidt pass when |r|^2 < kDgks * |r'|^2 (DGKS)
 constexpr int kMaxRestarts = 8;
-constexpr int kBatch = 8192;       // chunks per workspace batch
+constexpr int kBatch = 16384;      // chunks per workspace batch (a d = 1e7 layer at itv 1000 in one)
 constexpr int kMisc = 8;           // per-chunk scalars: [0] np.average scale, [1] ex_noregret step
 
 // per-iteration diagnostics of chunk 0 (sra_filter_debug_f32): FNP weights
@@ -378,6 +379,8 @@ struct SolveArgs {
   int* fb_list;      // chunks handed to the re-orthogonalising fallback
   int* fb_count;
   int* trace;        // optional [nb][1 + 2 FNP] decision trace (sra_filter_trace_f32), batch-relative
+  int first_off;     // lanczos_solve_kernel: first check at (previous iteration's steps) + first_off
+  int max_adv;       // lanczos_solve_kernel: checks at most this many steps apart
 };
 
 // Decision trace of one chunk (sra_filter_trace_f32): [0] iterations completed
@@ -1821,7 +1824,12 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       double tscale = 0.0;
       long long tcheck = 0;
       int trounds = 0;
-      for (int attempt = 0; attempt < 2 && !converged; ++attempt) {
+      // attempt 0: plain Lanczos; 1: after a ghost, again with dense checks;
+      // 2: with full re-orthogonalisation against the stored basis (the rare
+      // chunk whose top pair plain Lanczos cannot resolve is finished here, in
+      // its own iteration, instead of being redone on the fallback kernel)
+      for (int attempt = 0; attempt < 3 && !converged; ++attempt) {
+        const bool reorth = attempt == 2;
         double rt;
         {
           const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
@@ -1836,8 +1844,9 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         tscale = 0.0;
         // incremental Gershgorin bounds of T: rows 0 .. j-2 final, plus row j-1
         double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
-        const int adv_max = attempt == 0 ? kMaxAdvance : 1;
-        int next_check = attempt == 0 ? (m_hint - 8 > 4 ? m_hint - 8 : 4) : (m_retry > 4 ? m_retry : 4);
+        const int adv_max = attempt == 1 ? 1 : A.max_adv;
+        const int first = m_hint + A.first_off > 4 ? m_hint + A.first_off : 4;
+        int next_check = attempt == 1 ? (m_retry > 4 ? m_retry : 4) : first;
         int m_a = -1, m_last = 4, m_pre = 4;
         double res_a = 0.0;
         bool ghost = false;
@@ -1887,10 +1896,14 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
                 zbest = zcur;
                 zcur ^= 1;
               }
-              ghost = res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
+              ghost = !reorth && res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
               const bool out_of_steps = j == MMAX;
               if (ghost || out_of_steps) {
                 if (tid == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
+                if (!ghost && attempt < 2) {   // out of steps: straight on to the re-orthogonalising attempt
+                  ghost = true;
+                  attempt = 1;
+                }
                 m_retry = m_pre;
                 break;
               }
@@ -1918,8 +1931,40 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
           if (own) Vb[j * FNP + row] = q;
           const double mq = y * ib;
           reduce2(own ? q * mq : 0.0, 0.0, o, 1);
-          const double aj = o[0];
-          const double r = mq - aj * q - (j > 0 ? bet * qprev : 0.0);
+          double aj = o[0];
+          double r = mq - aj * q - (j > 0 ? bet * qprev : 0.0);
+          if (reorth) {
+            // classical Gram-Schmidt against q_0 .. q_j (the own lanes' basis
+            // entries, read back by both lanes of the row after the stores
+            // landed), a second pass when |r|^2 drops below half (DGKS); alpha
+            // takes the q_j coefficients
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            constexpr int HS = MMAX + 2;
+            double* hs = cscr;            // [4][HS] per-wave sums
+            double* hb = cscr + 4 * HS;   // [HS] block sums
+            for (int pass = 0; pass < 2; ++pass) {
+              const int nh = pass == 0 ? j + 2 : j + 1;
+              for (int qq = 0; qq < nh; ++qq) {
+                double v = own ? (qq <= j ? Vb[qq * FNP + row] * r : r * r) : 0.0;
+                v = wave_sum(v);
+                if (lane == 0) hs[wave * HS + qq] = v;
+              }
+              lds_barrier();
+              if (tid < nh) hb[tid] = (hs[tid] + hs[HS + tid]) + (hs[2 * HS + tid] + hs[3 * HS + tid]);
+              lds_barrier();
+              double upd = 0.0, hn2 = 0.0;
+              for (int qq = 0; qq <= j; ++qq) {
+                const double hv = hb[qq];
+                upd = fma(hv, Vb[qq * FNP + row], upd);
+                hn2 = fma(hv, hv, hn2);
+              }
+              r -= upd;
+              aj += hb[j];
+              const bool again = pass == 0 && hb[j + 1] - hn2 < kDgks * hb[j + 1];
+              lds_barrier();   // hb / hs are rewritten by the next pass or check
+              if (!again) break;
+            }
+          }
           if (tid == 0) trw[2 * j] = aj;
           a_last = aj;
           tscale = fmax(tscale, fabs(aj));
@@ -2707,8 +2752,12 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("noregret_pre_kernel");
       if (rc) return rc;
     }
+    // check schedule of the plain solver (SRA_FCHECK / SRA_FADV: A/B runs only)
+    static const int first_off = [] { const char* e = getenv("SRA_FCHECK"); return e && *e ? atoi(e) : -8; }();
+    static const int max_adv = [] { const char* e = getenv("SRA_FADV"); return e && *e ? atoi(e) : kMaxAdvance; }();
     SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
-                 trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr};
+                 trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr, first_off,
+                 max_adv > 0 ? max_adv : 1};
     SRA_HIP(hipMemsetAsync(fbc, 0, 8 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
     if (mode == 1) {

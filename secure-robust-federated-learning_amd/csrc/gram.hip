@@ -64,11 +64,11 @@ __device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, bf16x8& h
   }
 }
 
-template <int NB, int WAVES = 4>
+template <int NB, int WAVES = 4, int STG = 0>
 struct GramCfg {
   static constexpr int NP = 32 * NB;
   static constexpr int THREADS = 64 * WAVES;
-  static constexpr int STAGE = NB <= 4 ? 128 : 64;                // coordinates per stage
+  static constexpr int STAGE = STG ? STG : (NB <= 4 ? 128 : 64);  // coordinates per stage
   static constexpr int ROWPAD = STAGE + 4;                       // LDS row stride (floats)
   static constexpr int T = NB * (NB + 1) / 2;                    // upper-triangle tiles
   // tile groups: 4 waves -> keep <= 176 accumulators per wave; 8 waves (two
@@ -105,9 +105,9 @@ struct GramCfg {
   static constexpr int lds_floats = 2 * BUF + PART + 2 * STAGE;  // stage buffers, partials, means
 };
 
-template <int NB, int WAVES>
+template <int NB, int WAVES, int STG = 0>
 int gram_slab_floats_t(int64_t num_wg) {
-  using C = GramCfg<NB, WAVES>;
+  using C = GramCfg<NB, WAVES, STG>;
   return static_cast<int>(num_wg * C::WK * C::T * 1024);
 }
 
@@ -126,11 +126,11 @@ __device__ __forceinline__ float sum_lanes_16_32(float x) {
 // path below).  shift != nullptr replaces the per-stage client mean by a
 // fixed per-coordinate shift (the mean over ALL N clients), so the pairs'
 // Grams are centred alike and assemble into one matrix.
-template <int NB, int WAVES, bool VEC, int TG>
+template <int NB, int WAVES, bool VEC, int TG, int STG>
 __device__ __forceinline__ void gram_body(const float* __restrict__ X, const float* __restrict__ X2, int split, int n,
                                           int64_t d, int64_t ldx, const float* __restrict__ shift, int64_t chunk,
                                           float* __restrict__ slab, float* lds) {
-  using C = GramCfg<NB, WAVES>;
+  using C = GramCfg<NB, WAVES, STG>;
   constexpr int STAGE = C::STAGE;
   constexpr int tg = TG;
   // LDS carve-up (pointers derived arithmetically from the __shared__ base so
@@ -298,16 +298,16 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
   }
 }
 
-template <int NB, int WAVES, bool VEC>
+template <int NB, int WAVES, bool VEC, int STG = 0>
 __global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* __restrict__ X,
                                                                   const float* __restrict__ X2, int split, int n,
                                                                   int64_t d, int64_t ldx,
                                                                   const float* __restrict__ shift, int64_t chunk,
                                                                   float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int WT = GramCfg<NB, WAVES>::WT;
+  constexpr int WT = GramCfg<NB, WAVES, STG>::WT;
   const int tg = (threadIdx.x >> 6) % WT;  // wave-uniform
-#define SRA_GB(TGV) gram_body<NB, WAVES, VEC, TGV>(X, X2, split, n, d, ldx, shift, chunk, slab, lds)
+#define SRA_GB(TGV) gram_body<NB, WAVES, VEC, TGV, STG>(X, X2, split, n, d, ldx, shift, chunk, slab, lds)
   if (tg == 0) SRA_GB(0);
   if constexpr (WT > 1) if (tg == 1) SRA_GB(1);
   if constexpr (WT > 2) {
@@ -431,11 +431,11 @@ struct GramPair {
   int split, off_a, off_b, ldg, write_aa, write_bb;
 };
 
-template <int NB, int WAVES>
+template <int NB, int WAVES, int STG = 0>
 static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s,
                            const GramPair* pr = nullptr) {
-  using C = GramCfg<NB, WAVES>;
-  const int nwg = gram_num_wg(d);
+  using C = GramCfg<NB, WAVES, STG>;
+  const int nwg = gram_num_wg(d) * (STG == 64 && NB <= 4 ? 2 : 1);
   const int64_t chunk = cdiv(cdiv(d, nwg), C::STAGE) * C::STAGE;
   const size_t lds = sizeof(float) * C::lds_floats;
   const float* X2 = pr ? pr->X2 : X;
@@ -444,19 +444,19 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
   const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(X2) & 15) == 0);
   if (vec) {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true>),
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true, STG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split, n,
-                       d, ldx, shift, chunk, slab);
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true, STG>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split,
+                       n, d, ldx, shift, chunk, slab);
   } else {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, false>),
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, false, STG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split, n,
-                       d, ldx, shift, chunk, slab);
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false, STG>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2,
+                       split, n, d, ldx, shift, chunk, slab);
   }
   int rc = launch_status("gram_partial_kernel");
   if (rc) return rc;
-  double* partial = reinterpret_cast<double*>(slab + static_cast<size_t>(gram_slab_floats_t<NB, WAVES>(nwg)));
+  double* partial = reinterpret_cast<double*>(slab + static_cast<size_t>(gram_slab_floats_t<NB, WAVES, STG>(nwg)));
   hipLaunchKernelGGL((gram_reduce1_kernel<NB>), dim3(cdiv(C::T * 1024, 256), kRedGroups), dim3(256), 0, s, slab,
                      static_cast<int64_t>(nwg) * C::WK, partial);
   rc = launch_status("gram_reduce1_kernel");
@@ -473,6 +473,12 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
 template <int NB>
 static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s,
                           const GramPair* pr = nullptr) {
+  // SRA_GRAM_STAGE64=1: 64-coordinate stages for N <= 128, half the LDS, two
+  // workgroups per CU (A/B runs)
+  static const int st64 = [] { const char* e = getenv("SRA_GRAM_STAGE64"); return e && *e ? atoi(e) : 0; }();
+  if constexpr (NB <= 4) {
+    if (st64 == 1 && gram_waves(NB) == 4) return launch_gram_nbw<NB, 4, 64>(X, n, d, ldx, G, slab, s, pr);
+  }
   if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
   return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s, pr);
 }
@@ -485,7 +491,7 @@ size_t gram_workspace_bytes(int n, int64_t d) {
   // the 256-row pair layout plus the d-vector shift
   const int nb = static_cast<int>(cdiv(n > 256 ? 256 : n, 32));
   const int T = nb * (nb + 1) / 2;
-  const size_t base = sizeof(float) * static_cast<size_t>(gram_num_wg(d)) * 8 * T * 1024 +
+  const size_t base = sizeof(float) * static_cast<size_t>(gram_num_wg(d)) * 2 * 8 * T * 1024 +
                       sizeof(double) * static_cast<size_t>(kRedGroups) * T * 1024;
   return n > 256 ? base + 256 + sizeof(float) * static_cast<size_t>(d) : base;
 }

@@ -20,7 +20,6 @@ for rec in fixtures(func="bulyan"):
     x = rec["x"].reshape(rec["x"].shape[0], -1)
     f = rec["params"]["f"]
     if rec["name"] == target:
-        os.environ["SRA_DEBUG_ROWS"] = "1"
         xs = [rec["x"][i] for i in range(rec["x"].shape[0])]
         got = gre.bulyan(xs, f, rec["params"]["aggsubfunc"])
         torch.cuda.synchronize()
