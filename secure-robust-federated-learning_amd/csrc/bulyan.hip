@@ -558,10 +558,27 @@ __device__ double bulyan_window_mean(Col&& s, int theta, int keep, int p0) {
     if (taken) lo = mid;
     else hi = mid - 1;
   }
-  double acc = static_cast<double>(run) * c;
-  for (int p = pl - lo; p < pl; ++p) acc += static_cast<double>(s(p));
-  for (int p = pr + 1; p <= pr + k - lo; ++p) acc += static_cast<double>(s(p));
-  return acc / static_cast<double>(keep);
+  // every partial sum is exact (the caller's span test), so the window is
+  // summed as four independent chains: the order is immaterial
+  double a0 = static_cast<double>(run) * c, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  const int w0 = pl - lo, w1 = pr + k - lo;   // the window minus the run: [w0, pl) and (pr, w1]
+  int p = w0;
+  for (; p + 3 < pl; p += 4) {
+    a0 += static_cast<double>(s(p));
+    a1 += static_cast<double>(s(p + 1));
+    a2 += static_cast<double>(s(p + 2));
+    a3 += static_cast<double>(s(p + 3));
+  }
+  for (; p < pl; ++p) a0 += static_cast<double>(s(p));
+  p = pr + 1;
+  for (; p + 3 <= w1; p += 4) {
+    a0 += static_cast<double>(s(p));
+    a1 += static_cast<double>(s(p + 1));
+    a2 += static_cast<double>(s(p + 2));
+    a3 += static_cast<double>(s(p + 3));
+  }
+  for (; p <= w1; ++p) a1 += static_cast<double>(s(p));
+  return ((a0 + a1) + (a2 + a3)) / static_cast<double>(keep);
 }
 
 constexpr int kFinalMaxTheta = 128;
@@ -696,166 +713,156 @@ __global__ void __launch_bounds__(64) bulyan_listed_kernel(const float* __restri
   }
 }
 
-// One wave per workgroup, one lane per coordinate, registers only (round 3).
-// The theta selected values are gathered in selection order (row indices
-// broadcast from VGPRs by readlane, loaded with every lane active) and kept
-// twice: as loaded (o) and sorted by the register network (v).  Then
-//   * the magnitude span: when every partial sum of values and of
-//     |differences| is exact in fp64 the result does not depend on summation
-//     order (else the column is listed);
-//   * an even theta's tie between the two middle values is decided from o:
-//     their totals are equal, so the first selection-order index holding
-//     either wins, as np.argmin does (round 2 re-read the column for this: 2x
-//     the algorithmic fetch);
-//   * the window of the keep values nearest the centre c: it starts at the
-//     first L in [max(0, p0 - keep + 1), min(p0, theta - keep)] whose left end
-//     is not strictly farther than the value just past its right end,
-//     c - v[L] <= v[L + keep] - c (the reference's walk takes the left value on
-//     ties); the predicate is monotone in L, so L* = Lmin + the number of L
-//     where it fails.  v[L + keep] for every static L comes from a copy of v
-//     shifted by the launch-uniform keep one power of two at a time (uniform
-//     branches), the comparisons and the window sum in exact fp64.
-// No LDS, so nothing serialises the waves (round 2 shared one LDS tile per
-// four waves by turns: 80 % of the wave time waiting).  Columns failing the
-// span test, or holding a NaN or an infinity, go to bulyan_listed_kernel.
+// Four waves per block, one lane per coordinate.  The theta selected values
+// are gathered in selection order (row indices broadcast from VGPRs by
+// readlane) and sorted in registers.  The sorted column goes through ONE LDS
+// tile per block that the four waves take in turn (a barrier per turn), so
+// LDS does not cap the occupancy (round 1's per-wave tile allowed 6 waves per
+// CU: 5.3 ms at theta = 88, d = 1e7).  In its turn a wave checks the column's
+// magnitude span -- when every partial sum of values and of |differences| is
+// exact in fp64 the result does not depend on summation order -- and finds
+// the windows of the centre candidates by bisection.  The even-theta
+// tie-break between the two middle values re-reads the column in selection
+// order: their totals are then equal, so the first index holding either
+// value decides, as np.argmin does.  Columns failing the span test, or
+// holding a NaN or an infinity, go to bulyan_listed_kernel.
 template <int P>  // theta in (P - 16, P]
-__global__ void __launch_bounds__(64, P <= 96 ? 2 : 1) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
-                                                             const int* __restrict__ rows, int nrows_s, int theta,
-                                                             int keep, int64_t d, double* __restrict__ out,
-                                                             int* __restrict__ nf_count, int64_t* __restrict__ nf_list) {
+__global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
+                                                           const int* __restrict__ rows, int nrows_s, int theta,
+                                                           int keep,
+                                                           int64_t d, double* __restrict__ out,
+                                                           int* __restrict__ nf_count, int64_t* __restrict__ nf_list) {
   constexpr int P2 = next_pow2(P);
-  const int t = threadIdx.x;
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * 64;
-  const int64_t rem = d - base;
-  const int tl = t < rem ? t : static_cast<int>(rem - 1);
-  const int64_t j = base + tl;
+  __shared__ float col[P][64];
+  const int t = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 + wave * 64;
+  const int64_t rem = d - base;   // may be <= 0 for the last block's trailing waves
+  const int tl = rem <= 0 ? 0 : (t < rem ? t : static_cast<int>(rem - 1));
+  const int64_t j = rem <= 0 ? d - 1 : base + tl;
   constexpr int RW = (P + 63) / 64;
   int rl[RW];
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
     const int li = 64 * q + t;
     rl[q] = rows[li < theta ? li : theta - 1];
-    asm volatile("" : "+v"(rl[q]));
   }
+  const int64_t jb = j - tl;   // this wave's first coordinate (clamped)
   const unsigned off = static_cast<unsigned>(tl) * 4u;
   constexpr int kFirstPad = P > 16 ? P - 16 : 0;
-  float o[P];          // the column in selection order
-  bool nonfinite = false;
-#pragma unroll
-  for (int i = 0; i < P; ++i) {
-    const int row = checked_row(__builtin_amdgcn_readlane(rl[i / 64], i % 64), nrows_s);
-    const char* rp = uniform_ptr(reinterpret_cast<const char*>(S + static_cast<int64_t>(row) * lds_ + base));
-    const float x = ld_lane(rp, off);
-    __builtin_amdgcn_sched_barrier(0);   // one row address at a time in SGPRs
-    const bool real = i < kFirstPad || i < theta;
-    o[i] = real ? x : __builtin_inff();
-    nonfinite |= real && !__builtin_isfinite(x);
-  }
-  float v[P2];
-#pragma unroll
-  for (int i = 0; i < P; ++i) v[i] = o[i];
-  if (__builtin_amdgcn_ballot_w64(nonfinite) != 0) {
-#pragma unroll
-    for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
-  }
-  network_fast<P2, P, 0, P>(v);
-  const bool even = (theta & 1) == 0;
-  const float cl = pick_mid<P, P2>(v, even ? theta / 2 - 1 : (theta - 1) / 2);
-  const float cu = pick_mid<P, P2>(v, theta / 2);
-  // magnitude span: |value| bits compare as unsigned
-  // integers; the +inf padding never wins the minimum and the largest
-  // magnitude sits at one end of the sorted column
-  bool exact = true;
-  {
-    unsigned mnb = 0xffffffffu;   // (smallest nonzero |value| bits) - 1
+  auto load_col = [&](float (&v)[P2], bool& nonfinite) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-      const unsigned ab = (__builtin_bit_cast(unsigned, v[i]) & 0x7fffffffu) - 1u;   // 0 wraps: ignored
-      mnb = ab < mnb ? ab : mnb;
+      const int row = checked_row(__builtin_amdgcn_readlane(rl[i / 64], i % 64), nrows_s);
+      const char* rp = uniform_ptr(reinterpret_cast<const char*>(S + static_cast<int64_t>(row) * lds_ + jb));
+      const float x = ld_lane(rp, off);
+      // one row address at a time in SGPRs (hoisting all of them spills)
+      __builtin_amdgcn_sched_barrier(0);
+      // rows below P - 16 always exist (theta > P - 16): no per-row predicate
+      const bool real = i < kFirstPad || i < theta;
+      v[i] = real ? x : __builtin_inff();
+      nonfinite |= real && !__builtin_isfinite(x);
     }
-    const float top = fmaxf(-v[0], pick_hi<P, P2>(v, theta - 1));
-    const unsigned mxb = top < 0.f ? 0u : __builtin_bit_cast(unsigned, top);
-    if (mnb != 0xffffffffu) {
-      const int emx = static_cast<int>(mxb >> 23) - 126;   // max|x| < 2^emx
-      const int ebn = static_cast<int>((mnb + 1u) >> 23);
-      const int ulp = (ebn > 0 ? ebn : 1) - 150;          // ulp(min nonzero |x|) = 2^ulp
-      exact = (emx + 8) - ulp <= 53;
+  };
+
+  const bool even = (theta & 1) == 0;
+  float cl, cu;            // centre candidates: the two middle values (even theta) or the median (cl)
+  bool nonfinite = false;
+  {
+    float v[P2];
+    load_col(v, nonfinite);
+    if (__builtin_amdgcn_ballot_w64(nonfinite) != 0) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
     }
-  }
-  // even theta, two distinct middle values: the first selection-order index
-  // holding either decides (padding slots hold +inf, never a finite centre)
-  bool upper = false;
-  if (even && cu != cl) {
-    int fl = theta, fu = theta;
+    network_fast<P2, P, 0, P>(v);
+    cl = pick_mid<P, P2>(v, even ? theta / 2 - 1 : (theta - 1) / 2);
+    cu = pick_mid<P, P2>(v, theta / 2);
+    // magnitude span: every value, |x - y| and partial sum of <= 128 of them
+    // is a multiple of ulp(smallest nonzero |value|) below 256 max|value|;
+    // exact in fp64 when that spans <= 53 bits.  |value| bits compare as
+    // unsigned integers; the +inf padding never wins the minimum, and the
+    // maximum magnitude is at one end of the sorted column.
+    bool exact = true;   // all sums exact in fp64
+    {
+      unsigned mnb = 0xffffffffu;   // (smallest nonzero |value| bits) - 1
 #pragma unroll
-    for (int i = P - 1; i >= 0; --i) {
-      fl = o[i] == cl ? i : fl;
-      fu = o[i] == cu ? i : fu;
+      for (int i = 0; i < P; ++i) {
+        const unsigned ab = (__builtin_bit_cast(unsigned, v[i]) & 0x7fffffffu) - 1u;   // 0 wraps: ignored
+        mnb = ab < mnb ? ab : mnb;
+      }
+      const unsigned mxb = fmaxf(-v[0], pick_hi<P, P2>(v, theta - 1)) < 0.f
+                               ? 0u : __builtin_bit_cast(unsigned, fmaxf(-v[0], pick_hi<P, P2>(v, theta - 1)));
+      if (mnb != 0xffffffffu) {
+        const int emx = static_cast<int>(mxb >> 23) - 126;   // max|x| < 2^emx
+        const int ebn = static_cast<int>((mnb + 1u) >> 23);
+        const int ulp = (ebn > 0 ? ebn : 1) - 150;          // ulp(min nonzero |x|) = 2^ulp
+        exact = (emx + 8) - ulp <= 53;
+      }
     }
-    upper = fu < fl;
-  }
-  const int p0 = even ? theta / 2 - 1 : (theta - 1) / 2;   // the lower centre; the upper one is p0 + 1
-  const double c = static_cast<double>(upper ? cu : cl);
-  // w[L] = v[L + keep] (+inf past the column): v shifted by the uniform keep
-  float w[P];
+    // this wave's turn with the LDS tile: wave w works between the block's
+    // barriers w + 1 and w + 2 (every wave passes four), so the sorted values
+    // are dead once stored and do not share registers with the window search
+    double res_l = 0.0, res_u = 0.0;
+#pragma unroll 1
+    for (int w = 0; w <= wave; ++w) __syncthreads();
 #pragma unroll
-  for (int i = 0; i < P; ++i) w[i] = v[i];
-#pragma unroll
-  for (int b = 7; b >= 0; --b) {
-    if (keep & (1 << b)) {   // launch-uniform: a scalar branch
-#pragma unroll
-      for (int i = 0; i < P; ++i) w[i] = i + (1 << b) < P ? w[i + (1 << b)] : __builtin_inff();
+    for (int i = 0; i < P; ++i) col[i][t] = v[i];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    auto s = [&](int p) -> float { return col[p][t]; };
+    if (keep == 0) {
+      // the mean of an empty slice: NaN for every column, written below
+    } else if (nonfinite) {
+      // a NaN or an infinity changes which value is the centre (see
+      // bulyan_stage_generic): listed for bulyan_listed_kernel
+      if (rem > 0 && t < rem) nf_list[atomicAdd(nf_count, 1)] = 2 * j + 1;
+    } else {
+      if (exact) {
+        res_l = bulyan_window_mean(s, theta, keep, even ? theta / 2 - 1 : (theta - 1) / 2);
+        if (even && cu != cl) res_u = bulyan_window_mean(s, theta, keep, theta / 2);
+      } else if (rem > 0 && t < rem) {
+        // rounding decides the centre and the order of the sums
+        nf_list[atomicAdd(nf_count, 1)] = 2 * j;
+      }
     }
-  }
-  // the candidate starts of both centres together, [lmin_u, lmax_u] (wave-
-  // uniform bounds, re-materialised in SGPRs so the per-slot conditions are
-  // scalar branches); the predicate fails on a prefix of it, so the lane's
-  // start is that prefix's end clamped to its own centre's range
-  const int pc = upper ? p0 + 1 : p0;
-  int lmin_u = p0 - keep + 1 > 0 ? p0 - keep + 1 : 0;
-  int lmax_u = (p0 + 1 < theta - keep ? p0 + 1 : theta - keep);
-  asm volatile("" : "+s"(lmin_u), "+s"(lmax_u));
-  const int lmin = pc - keep + 1 > 0 ? pc - keep + 1 : 0;
-  const int lmax = pc < theta - keep ? pc : theta - keep;
-  const double c2 = 2.0 * c;
-  int cnt = 0;
+#pragma unroll 1
+    for (int w = wave + 1; w < 4; ++w) __syncthreads();
+    // no early return from here on: the tie-break's gather broadcasts row
+    // indices across lanes (readlane), which must not read the register
+    // slots of lanes that left (the compiler may have copied the row list
+    // under a partial exec mask, leaving stale values there)
+    bool write = rem > 0 && t < rem && (keep == 0 || (!nonfinite && exact));   // else listed for bulyan_listed_kernel
+    double result = res_l;
+    bool tie = false;
+    if (keep == 0) result = __builtin_nan("");   // mean of an empty slice
+    else if (even && cu != cl) tie = true;
+    if (__builtin_amdgcn_ballot_w64(write && tie) != 0) {   // wave-uniform: every lane active
+      // even theta, two distinct middle values: np.argmin over the totals.
+      // The row list is reloaded here, with every lane active, and kept opaque
+      // (the first gather's row addresses are then not held live for reuse)
 #pragma unroll
-  for (int L = 0; L < P; ++L) {
-    if (L >= lmin_u && L <= lmax_u) {
-      // c - v[L] > w[L] - c, exact in fp64
-      cnt += static_cast<double>(v[L]) + static_cast<double>(w[L]) < c2 ? 1 : 0;
-    }
-  }
-  const int lx = lmin_u + cnt;
-  const int ls = lx < lmin ? lmin : (lx > lmax ? lmax : lx);
-  int hi_u = lmax_u + keep;
-  asm volatile("" : "+s"(hi_u));
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int q = 0; q < RW; ++q) {
+        const int li = 64 * q + t;
+        rl[q] = rows[li < theta ? li : theta - 1];
+        asm volatile("" : "+v"(rl[q]));
+      }
+      float o[P2];
+      bool dummy = false;
+      load_col(o, dummy);
+      int fl = theta, fu = theta;
 #pragma unroll
-  for (int i = 0; i < P; ++i) {
-    if (i >= lmin_u && i < hi_u) {
-      const double x = (i >= ls && i < ls + keep) ? static_cast<double>(v[i]) : 0.0;
-      if ((i & 3) == 0) a0 += x;
-      else if ((i & 3) == 1) a1 += x;
-      else if ((i & 3) == 2) a2 += x;
-      else a3 += x;
+      for (int i = P - 1; i >= 0; --i) {
+        // padding slots hold +inf, never a (finite) centre value
+        fl = o[i] == cl ? i : fl;
+        fu = o[i] == cu ? i : fu;
+      }
+      // exact sums: the two totals are equal (the middle values split the
+      // column in halves), so np.argmin takes the first index holding either
+      if (tie) result = fl < fu ? res_l : res_u;
     }
+    if (write) out[base + t] = result;
   }
-  if (rem <= 0 || t >= rem) return;
-  if (keep == 0) {   // the mean of an empty slice
-    out[j] = __builtin_nan("");
-    return;
-  }
-  if (nonfinite) {   // a NaN or an infinity changes which value is the centre
-    nf_list[atomicAdd(nf_count, 1)] = 2 * j + 1;
-    return;
-  }
-  if (!exact) {      // rounding decides the centre and the order of the sums
-    nf_list[atomicAdd(nf_count, 1)] = 2 * j;
-    return;
-  }
-  // exact: every partial sum is exact, so the grouping of the four is immaterial
-  out[j] = ((a0 + a1) + (a2 + a3)) / static_cast<double>(keep);
 }
 
 // ---------------------------------------------------------------------------
@@ -1093,8 +1100,8 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows
   int rc = SRA_ERR_UNSUPPORTED;
 #define SRA_FIN(PP)                                                                                              \
   case PP:                                                                                                       \
-    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(cdiv(d, 64)), dim3(64), 0, s, S,                            \
-                       lds_, rows, nrows_s, theta, keep, d, out, nf_count, nf_list);                             \
+    hipLaunchKernelGGL((bulyan_final_kernel<PP>), dim3(cdiv(d, 256)), dim3(256), 0, s, S, lds_, rows, nrows_s,   \
+                       theta, keep, d, out, nf_count, nf_list);                                                  \
     rc = launch_status("bulyan_final_kernel");                                                                   \
     if (rc) return rc;                                                                                           \
     hipLaunchKernelGGL((bulyan_listed_kernel<PP>), dim3(256), dim3(64), 0, s, S, lds_, rows, nrows_s, theta, keep,  \

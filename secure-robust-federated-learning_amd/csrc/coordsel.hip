@@ -357,7 +357,11 @@ __device__ __forceinline__ float from_lane(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), ctrl, 0xF, 0xF, false));
 }
 
-template <int L, int MODE, int NX = 0, int BX = -1>
+// NT: streaming (non-temporal) row loads.  A wave's load instruction covers
+// 16 coordinates = half a 128-byte line per row, the other half belongs to
+// the neighbouring wave of the block, so the N = 512 launches use plain loads
+// (SRA_QUAD_NT=1 restores streaming loads for A/B runs).
+template <int L, int MODE, int NX = 0, int BX = -1, bool NT = true>
 __global__ void __launch_bounds__(256) select_quad_kernel(const float* __restrict__ X, int n_rt, int64_t d,
                                                          int64_t ldx, int lo_rt, int hi_rt, float* __restrict__ out) {
   static_assert(L == 2 || L == 4, "2 or 4 lanes per coordinate");
@@ -388,7 +392,8 @@ __global__ void __launch_bounds__(256) select_quad_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < 128; ++i) {
     if (kExactN ? (L * i + L - 1 < NX) : (L * i + L - 1 < n)) {     // wave-uniform: all L rows real
-      v[i] = __builtin_nontemporal_load(reinterpret_cast<gfloat*>(rp + off));
+      if constexpr (NT) v[i] = __builtin_nontemporal_load(reinterpret_cast<gfloat*>(rp + off));
+      else v[i] = *reinterpret_cast<gfloat*>(rp + off);
     } else {                                                          // tail: clamp the row, then pad
       const int row = L * i + h;
       const int rr = row < n ? row : n - 1;
@@ -618,8 +623,16 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
   }
   if (quad_ok && n > 256 && n <= 512) {
     if (n == 512 && (MODE == kMedian || (lo == 51 && hi == 461))) {
-      hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51>), dim3(cdiv(d, 64)), dim3(256),
-                         0, s, X, n, d, ldx, lo, hi, out);
+      // plain loads: with streaming loads the half line a wave leaves for its
+      // neighbour was refetched (median 1.12x the algorithmic bytes, 7.03 ms;
+      // plain 1.00x, 6.83 ms at d = 1.25e7)
+      static const int nt = env_int("SRA_QUAD_NT", 0);
+      if (nt == 0)
+        hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51, false>), dim3(cdiv(d, 64)),
+                           dim3(256), 0, s, X, n, d, ldx, lo, hi, out);
+      else
+        hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51>), dim3(cdiv(d, 64)), dim3(256),
+                           0, s, X, n, d, ldx, lo, hi, out);
     } else {
       hipLaunchKernelGGL((select_quad_kernel<4, MODE>), dim3(cdiv(d, 64)), dim3(256), 0, s, X, n, d, ldx, lo, hi,
                          out);

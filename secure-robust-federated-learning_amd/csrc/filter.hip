@@ -381,6 +381,7 @@ struct SolveArgs {
   int* trace;        // optional [nb][1 + 2 FNP] decision trace (sra_filter_trace_f32), batch-relative
   int first_off;     // lanczos_solve_kernel: first check at (previous iteration's steps) + first_off
   int max_adv;       // lanczos_solve_kernel: checks at most this many steps apart
+  int warm;          // lanczos_solve_kernel, ex_noregret: warm start from the previous Ritz vector
 };
 
 // Decision trace of one chunk (sra_filter_trace_f32): [0] iterations completed
@@ -1773,6 +1774,11 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
     int clog_n = 0;
     int done = 0;
     int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
+    // ex_noregret damps the top direction gently, so the previous iteration's
+    // Ritz vector is a near-eigenvector of the next M: warm start from it
+    // (filterL2's next top vector is essentially new)
+    double u_prev = 0.0;
+    bool have_u = false;
 
     for (int it = 0; it < iters; ++it) {
       const long long t_it = dbg ? clock64() : 0;
@@ -1830,10 +1836,14 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       // its own iteration, instead of being redone on the fallback kernel)
       for (int attempt = 0; attempt < 3 && !converged; ++attempt) {
         const bool reorth = attempt == 2;
+        // ex_noregret's weights integrate every iteration's eigenvector (no
+        // removal resets them): the re-orthogonalising solver's bound there
+        const double acc_tol = MODE == 1 ? kResTol : kAccept;
         double rt;
+        const bool warm = MODE == 1 && A.warm && have_u && attempt == 0;
         {
           const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
-          rt = swi > 0.0 ? swi * hh : 0.0;
+          rt = swi > 0.0 ? (warm ? u_prev + 1e-3 * swi * hh : swi * hh) : 0.0;
         }
         if (own) xbuf[row] = rt;
         reduce2(own ? rt * rt : 0.0, 0.0, o, 1);
@@ -1845,7 +1855,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         // incremental Gershgorin bounds of T: rows 0 .. j-2 final, plus row j-1
         double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
         const int adv_max = attempt == 1 ? 1 : A.max_adv;
-        const int first = m_hint + A.first_off > 4 ? m_hint + A.first_off : 4;
+        const int first = warm ? 1 : (m_hint + A.first_off > 4 ? m_hint + A.first_off : 4);
         int next_check = attempt == 1 ? (m_retry > 4 ? m_retry : 4) : first;
         int m_a = -1, m_last = 4, m_pre = 4;
         double res_a = 0.0;
@@ -1879,7 +1889,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
               ++clog_n;
               hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
               theta_lb = lm;
-              if (res <= kAccept * fabs(lm) || breakdown) {
+              if (res <= acc_tol * fabs(lm) || breakdown) {
                 converged = true;
                 m_conv = m;
                 lam = lm;
@@ -1911,7 +1921,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
               double rate = rate_hint;
               if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
               if (rate < 0.0 && res > 0.0) {
-                const double need = log(kAccept * fabs(lm) / res) / rate;
+                const double need = log(acc_tol * fabs(lm) / res) / rate;
                 adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
               }
               m_a = m;
@@ -1994,6 +2004,8 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         if (qq < m_conv) u0 = fma(zb[qq], Vb[qq * FNP + row], u0);
         ui = swi > 0.0 ? u0 + u1 : 0.0;
       }
+      u_prev = ui;
+      have_u = true;
       m_hint = m_conv > 8 ? m_conv : 8;
       if (dbg && it < 256) {
         double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
@@ -2735,9 +2747,18 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<1, false>));
   SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
-  const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
-                           : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
+  const void* lsolve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
+                                       : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>))
+                                 : (dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<1, true>)
+                                       : reinterpret_cast<const void*>(&lanczos_solve_kernel<1, false>));
   SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLds)));
+  // ex_noregret stays on the re-orthogonalising kernel.  SRA_NOREGRET_PLAIN=1
+  // runs it on the plain solver with the in-kernel re-orthogonalising attempt
+  // (A/B only: 217 ms vs 327 ms at C4, the decisions agree but the C4 fixture
+  // chunk 1 lands 2.9e-3 of max from the reference, bound 2e-5, and two DBA
+  // fixtures miss rtol 1e-5; SRA_NOREGRET_WARM=1 also warm-starts it)
+  static const int noregret_plain = [] { const char* e = getenv("SRA_NOREGRET_PLAIN"); return e && *e ? atoi(e) : 0; }();
+  static const int noregret_warm = [] { const char* e = getenv("SRA_NOREGRET_WARM"); return e && *e ? atoi(e) : 0; }();
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
     GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws};
@@ -2757,16 +2778,21 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     static const int max_adv = [] { const char* e = getenv("SRA_FADV"); return e && *e ? atoi(e) : kMaxAdvance; }();
     SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
                  trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr, first_off,
-                 max_adv > 0 ? max_adv : 1};
+                 max_adv > 0 ? max_adv : 1, noregret_warm};
     SRA_HIP(hipMemsetAsync(fbc, 0, 8 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
-    if (mode == 1) {
-      // ex_noregret damps the top direction gently, so its top two eigenvalues
-      // close in (gaps ~1e-3 after a few iterations) and plain Lanczos stalls
-      // above the accuracy floor in a third of the chunks: every chunk goes to
-      // the re-orthogonalising solver
+    if (mode == 1 && noregret_plain == 0) {
+      // round 2: ex_noregret's top two eigenvalues close in (gaps ~1e-3 after a
+      // few iterations) and plain Lanczos without the re-orthogonalising
+      // attempt stalled above the accuracy floor in a third of the chunks:
+      // every chunk on the re-orthogonalising solver
       hipLaunchKernelGGL(list_all_kernel, dim3(cdiv(nb, 256)), dim3(256), 0, s, fbl, fbc, nb);
       rc = launch_status("list_all_kernel");
+      if (rc) return rc;
+    } else if (mode == 1) {
+      if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<1, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      else hipLaunchKernelGGL((lanczos_solve_kernel<1, false>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      rc = launch_status("lanczos_solve_kernel");
       if (rc) return rc;
     } else {
       if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<0, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);

@@ -41,3 +41,16 @@ for st in 0 1; do
 import csv
 for x in list(csv.DictReader(open('$OUT/prof_krum_$st/run_kernel_stats.csv')))[:3]: print('  ', x['Name'][:50], x['Calls'], float(x['AverageNs'])/1e6)"
 done
+timeout -k 10 120 tools/ubench/bin/check_bench > "$OUT/check_bench.txt" 2>&1 || { echo "check_bench failed"; tail -3 "$OUT/check_bench.txt"; }
+tail -12 "$OUT/check_bench.txt"
+for agg in median trimmedmean; do for nt in 1 0; do
+  SRA_QUAD_NT=$nt timeout -k 10 120 python3 "$R/bench.py" --warmup 2 --no-cpu --no-host --agg $agg --clients 512 --d 1.25e7 --steps 10 > "$OUT/q_${agg}_$nt.log" 2>&1 || { echo "quad bench failed"; tail -3 "$OUT/q_${agg}_$nt.log"; exit 1; }
+  echo "QUAD_NT=$nt $agg N=512 $(grep '"metric"' "$OUT/q_${agg}_$nt.log" | python3 -c "import json,sys; l=json.loads(sys.stdin.read()); print(l['ms_per_step'], l['roofline']['kernel_ms'], l['roofline']['frac'])")"
+  SRA_QUAD_NT=$nt timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcq_${agg}_$nt" -o run -- python3 "$R/bench.py" --warmup 0 --no-cpu --no-host --agg $agg --clients 512 --d 1.25e7 --steps 1 > "$OUT/pmcq_${agg}_$nt.log" 2>&1 || { echo "pmc failed"; exit 1; }
+  python3 - "$OUT/pmcq_${agg}_$nt" <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)
+v = [float(r['Counter_Value']) for r in csv.DictReader(open(f[0])) if 'select_quad' in r['Kernel_Name']]
+print("  quad launches %d, 2 x FETCH_SIZE per launch %.3f GB (algorithmic 25.65)" % (len(v), 2 * sum(v) / max(1, len(v)) * 1024 / 1e9))
+PY
+done; done
