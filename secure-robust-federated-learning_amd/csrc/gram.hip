@@ -126,7 +126,29 @@ __device__ __forceinline__ float sum_lanes_16_32(float x) {
 // path below).  shift != nullptr replaces the per-stage client mean by a
 // fixed per-coordinate shift (the mean over ALL N clients), so the pairs'
 // Grams are centred alike and assemble into one matrix.
-template <int NB, int WAVES, bool VEC, int TG, int STG>
+// sum of x over the 32 lanes of each wave half (xor butterfly: every lane of a
+// half ends with the same bits, since a + b == b + a exactly)
+__device__ __forceinline__ float sum_lanes_32(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), 0x101f));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), 0x201f));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), 0x401f));
+  return x;
+}
+
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+// PF: register stage sets in flight (2: the loads of stage s + 3 are issued
+// while stage s computes, two stages of MFMA work to cover HBM latency).
+// WM: every wave derives the column means of its own k-steps from the values
+// it reads for the MFMA (sum_lanes_32 over the 32 rows of a block, blocks in
+// a fixed order; waves sharing k-steps compute the same bits), so a stage
+// needs one barrier and no partial-sum pass.  WM requires shift == nullptr.
+template <int NB, int WAVES, bool VEC, int TG, int STG, int PF = 1, bool WM = false>
 __device__ __forceinline__ void gram_body(const float* __restrict__ X, const float* __restrict__ X2, int split, int n,
                                           int64_t d, int64_t ldx, const float* __restrict__ shift, int64_t chunk,
                                           float* __restrict__ slab, float* lds) {
@@ -159,12 +181,28 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
   // staging: thread t owns float4 column c4 = t % C4 of rows t / C4 + RSTEP * q
-  f32x4 stg[C::LOADS];
+  f32x4 stg[PF][C::LOADS];
   const int c4 = tid % C::C4;
   const int row0 = tid / C::C4;
 
-  auto load_stage = [&](int s) {
-    const int64_t k0 = (static_cast<int64_t>(s) * gridDim.x + blockIdx.x) * STAGE + 4 * c4;
+  // fast path (all NP rows present in X, the stage inside [0, d), 16-byte
+  // aligned rows): a wave-uniform row base per load plus one 32-bit lane
+  // offset (global_load with an SGPR base), no per-load guards
+  const bool rows_full = VEC && n >= C::NP && split >= C::NP &&
+                         static_cast<int64_t>(C::RSTEP - 1) * ldx * 4 + 4 * STAGE < (int64_t(1) << 31);
+  const uint32_t lane_off = static_cast<uint32_t>((static_cast<int64_t>(row0) * ldx + 4 * c4) * 4);
+  auto load_stage = [&](int s, auto setc) {
+    constexpr int P = decltype(setc)::value;
+    const int64_t kb = (static_cast<int64_t>(s) * gridDim.x + blockIdx.x) * STAGE;
+    if (rows_full && kb + STAGE <= k_end) {
+#pragma unroll
+      for (int q = 0; q < C::LOADS; ++q) {
+        const char* bq = reinterpret_cast<const char*>(X + static_cast<int64_t>(C::RSTEP * q) * ldx + kb);
+        stg[P][q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(bq + lane_off));
+      }
+      return;
+    }
+    const int64_t k0 = kb + 4 * c4;
 #pragma unroll
     for (int q = 0; q < C::LOADS; ++q) {
       const int row = row0 + C::RSTEP * q;
@@ -179,20 +217,22 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
           for (int e = 0; e < 4; ++e) v[e] = (k0 + e < k_end) ? p[e] : 0.f;
         }
       }
-      stg[q] = v;
+      stg[P][q] = v;
     }
   };
   // registers -> LDS stage buffer, plus this wave's column partial sums
   // (the 64 lanes of a wave cover C4/…: lanes with equal c4 are reduced by
   // swizzles, then lanes with lane < C4 own the wave's partial of 4 columns)
-  auto store_stage = [&](float* b, float* part) {
+  auto store_stage = [&](float* b, float* part, auto setc) {
+    constexpr int P = decltype(setc)::value;
     f32x4 colsum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < C::LOADS; ++q) {
       const int row = row0 + C::RSTEP * q;
-      if (row < C::NP) *reinterpret_cast<f32x4*>(b + row * C::ROWPAD + 4 * c4) = stg[q];
-      colsum += stg[q];
+      if (row < C::NP) *reinterpret_cast<f32x4*>(b + row * C::ROWPAD + 4 * c4) = stg[P][q];
+      if constexpr (!WM) colsum += stg[P][q];
     }
+    if constexpr (WM) return;
     if constexpr (C::C4 == 16) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) colsum[e] = sum_lanes_16_32(colsum[e]);
@@ -222,19 +262,25 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
   };
 
   if (nstage > 0) {
-    load_stage(0);
-    store_stage(bufp(0), part);
-    if (nstage > 1) load_stage(1);
+    load_stage(0, IC<0>{});
+    if constexpr (PF == 2) {
+      if (nstage > 1) load_stage(1, IC<1>{});
+    }
+    store_stage(bufp(0), part, IC<0>{});
+    if (nstage > PF) load_stage(PF, IC<0>{});
     __syncthreads();
-    stage_means(mup(0), 0);
-    __syncthreads();
+    if constexpr (!WM) {
+      stage_means(mup(0), 0);
+      __syncthreads();
+    }
   }
 
   const int r = lane & 31;
   const int h = lane >> 5;
   // rows >= n of the last block are zeroed after centring (their staged value is 0)
   const float last_mask = (32 * (NB - 1) + r) < n ? 1.f : 0.f;
-  for (int s = 0; s < nstage; ++s) {
+  auto step = [&](int s, auto parc) {
+    constexpr int SN = PF == 2 ? 1 - decltype(parc)::value : 0;   // register set of stage s + 1
     const float* b = bufp(s & 1);
     const float* mu = mup(s & 1);
     // ---- MFMA over this wave's 16-coordinate k-steps of the stage ----
@@ -242,14 +288,43 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
     for (int gi = 0; gi < C::KPW; ++gi) {
       const int g = kg + C::WK * gi;
       const int col = 16 * g + 8 * h;
-      const f32x4 mu0 = *reinterpret_cast<const f32x4*>(mu + col);
-      const f32x4 mu1 = *reinterpret_cast<const f32x4*>(mu + col + 4);
+      f32x4 mu0, mu1;
+      f32x4 raw0[NB], raw1[NB];
+      if constexpr (WM) {
+#pragma unroll
+        for (int blk = 0; blk < NB; ++blk) {
+          const float* rp = b + (32 * blk + r) * C::ROWPAD + col;
+          raw0[blk] = *reinterpret_cast<const f32x4*>(rp);
+          raw1[blk] = *reinterpret_cast<const f32x4*>(rp + 4);
+        }
+        mu0 = raw0[0];
+        mu1 = raw1[0];
+#pragma unroll
+        for (int blk = 1; blk < NB; ++blk) {
+          mu0 += raw0[blk];
+          mu1 += raw1[blk];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          mu0[e] = sum_lanes_32(mu0[e]) * inv_n;
+          mu1[e] = sum_lanes_32(mu1[e]) * inv_n;
+        }
+      } else {
+        mu0 = *reinterpret_cast<const f32x4*>(mu + col);
+        mu1 = *reinterpret_cast<const f32x4*>(mu + col + 4);
+      }
       bf16x8 fh[NB], fm[NB], fl[NB];
 #pragma unroll
       for (int blk = 0; blk < NB; ++blk) {
         const float* rp = b + (32 * blk + r) * C::ROWPAD + col;
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(rp) - mu0;
-        f32x4 a1 = *reinterpret_cast<const f32x4*>(rp + 4) - mu1;
+        f32x4 a0, a1;
+        if constexpr (WM) {
+          a0 = raw0[blk] - mu0;
+          a1 = raw1[blk] - mu1;
+        } else {
+          a0 = *reinterpret_cast<const f32x4*>(rp) - mu0;
+          a1 = *reinterpret_cast<const f32x4*>(rp + 4) - mu1;
+        }
         if (blk == NB - 1) {
           a0 *= last_mask;
           a1 *= last_mask;
@@ -272,14 +347,20 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
     }
     // ---- stage s+1 -> LDS (its registers were loaded one stage ahead) ----
     if (s + 1 < nstage) {
-      store_stage(bufp((s + 1) & 1), part);
-      if (s + 2 < nstage) load_stage(s + 2);
+      store_stage(bufp((s + 1) & 1), part, IC<SN>{});
+      if (s + 1 + PF < nstage) load_stage(s + 1 + PF, IC<SN>{});
     }
     __syncthreads();
-    if (s + 1 < nstage) {
-      stage_means(mup((s + 1) & 1), s + 1);
-      __syncthreads();
+    if constexpr (!WM) {
+      if (s + 1 < nstage) {
+        stage_means(mup((s + 1) & 1), s + 1);
+        __syncthreads();
+      }
     }
+  };
+  for (int s = 0; s < nstage; s += 2) {
+    step(s, IC<0>{});
+    if (s + 1 < nstage) step(s + 1, IC<1>{});
   }
 
   // ---- partial tiles -> slab[wg][kg][tile][32 x 32] (row-major) ----
@@ -298,7 +379,195 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
   }
 }
 
-template <int NB, int WAVES, bool VEC, int STG = 0>
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// Software-pipelined Gram for 96 < N <= 128 (NB = 4, four waves, the C3
+// shape).  Same arithmetic as gram_body<4, 4, VEC, 0, 1, true> (per-wave means
+// from a fixed butterfly, the exact three-way split, six bf16 MFMAs per tile
+// and k-step, tiles accumulated in the same k order), scheduled so that the
+// MFMA pipe is never left idle while the wave does its VALU work: each of the
+// 60 MFMAs of a k-step is followed by one small piece of the NEXT k-step's
+// preparation (its LDS reads, the column sums and butterfly, the centring and
+// split of one element pair) or of the stage traffic (one ds_write_b128 of the
+// next stage, one global load of the stage after), pinned in place by
+// sched_barrier.  Stage s:
+//   phase A: MFMA(k-step g0 of s) | prepare g1 of s (LDS s)   | store s+1 -> LDS
+//   barrier
+//   phase B: MFMA(k-step g1 of s) | prepare g0 of s+1 (LDS s+1) | load s+2
+// One barrier per stage: buffer s&1 is last read in phase A of stage s and next
+// written in phase A of stage s+1; buffer (s+1)&1 is written in phase A of s and
+// first read after the barrier.
+struct GramOps {
+  bf16x8 h[4], m[4], l[4];
+};
+
+// Host contract (launch_gram_nbw<..., PIPE>): N == 128, 16-byte aligned rows,
+// d a multiple of the 128-coordinate stage, so every load is a full, guard-free
+// float4 and the loop body is one basic block (no branch for sched_barrier to
+// stop at); past the last stage the loads re-read the last stage (discarded).
+__device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                               float* __restrict__ slab, float* lds) {
+  using C = GramCfg<4, 4, 0>;
+  constexpr int STAGE = C::STAGE;   // 128
+  constexpr int T = C::T;           // 10
+  static_assert(C::WK == 4 && C::KPW == 2 && C::LOADS == 16 && T == 10, "pipe layout");
+  auto bufp = [&](int which) { return lds + which * C::BUF; };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int kg = tid >> 6;
+  const int64_t ntiles = d / STAGE;
+  const int nstage = blockIdx.x < ntiles ? static_cast<int>(cdiv(ntiles - blockIdx.x, gridDim.x)) : 0;
+  const float inv_n = 1.0f / static_cast<float>(n);
+  const int r = lane & 31;
+  const int h = lane >> 5;
+
+  f32x16 acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+
+  f32x4 stg[C::LOADS];
+  const int c4 = tid % C::C4;
+  const int row0 = tid / C::C4;
+  const uint32_t lane_off = static_cast<uint32_t>((static_cast<int64_t>(row0) * ldx + 4 * c4) * 4);
+  auto stage_k = [&](int s) {
+    return (static_cast<int64_t>(s < nstage ? s : nstage - 1) * gridDim.x + blockIdx.x) * STAGE;
+  };
+  auto load_one = [&](int64_t kb, int q) {
+    const char* bq = reinterpret_cast<const char*>(X + static_cast<int64_t>(C::RSTEP * q) * ldx + kb);
+    stg[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(bq + lane_off));
+  };
+  auto store_one = [&](float* b, int q) {
+    *reinterpret_cast<f32x4*>(b + (row0 + C::RSTEP * q) * C::ROWPAD + 4 * c4) = stg[q];
+  };
+
+  // preparation of one k-step, split in 43 pieces
+  f32x4 raw0[4], raw1[4], mu0, mu1;
+  auto prep_piece = [&](auto pc, const float* b, int g, GramOps& o) {
+    constexpr int p = decltype(pc)::value;
+    const int col = 16 * g + 8 * h;
+    if constexpr (p < 4) {
+      const float* rp = b + (32 * p + r) * C::ROWPAD + col;
+      raw0[p] = *reinterpret_cast<const f32x4*>(rp);
+      raw1[p] = *reinterpret_cast<const f32x4*>(rp + 4);
+    } else if constexpr (p == 4) {
+      mu0 = ((raw0[0] + raw0[1]) + raw0[2]) + raw0[3];
+    } else if constexpr (p == 5) {
+      mu1 = ((raw1[0] + raw1[1]) + raw1[2]) + raw1[3];
+    } else if constexpr (p < 26) {
+      // butterfly: level-major, two of the eight values per piece
+      constexpr int q = p - 6;          // 0..19
+      constexpr int lvl = q / 4;        // 0..4
+      constexpr int v0 = 2 * (q % 4);   // values v0, v0 + 1 of (mu0, mu1)
+#pragma unroll
+      for (int vv = v0; vv < v0 + 2; ++vv) {
+        float x = vv < 4 ? mu0[vv] : mu1[vv - 4];
+        int xi = __builtin_bit_cast(int, x);
+        int yi;
+        if constexpr (lvl == 0) yi = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+        else if constexpr (lvl == 1) yi = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+        else if constexpr (lvl == 2) yi = __builtin_amdgcn_ds_swizzle(xi, 0x101f);
+        else if constexpr (lvl == 3) yi = __builtin_amdgcn_ds_swizzle(xi, 0x201f);
+        else yi = __builtin_amdgcn_ds_swizzle(xi, 0x401f);
+        x += __builtin_bit_cast(float, yi);
+        if (vv < 4) mu0[vv] = x; else mu1[vv - 4] = x;
+      }
+    } else if constexpr (p == 26) {
+      mu0 *= inv_n;
+      mu1 *= inv_n;
+    } else if constexpr (p < 43) {
+      // centre + split one element pair of one block
+      constexpr int blk = (p - 27) / 4;
+      constexpr int e2 = (p - 27) % 4;
+      float x0 = e2 < 2 ? raw0[blk][2 * e2] - mu0[2 * e2] : raw1[blk][2 * e2 - 4] - mu1[2 * e2 - 4];
+      float x1 = e2 < 2 ? raw0[blk][2 * e2 + 1] - mu0[2 * e2 + 1] : raw1[blk][2 * e2 - 3] - mu1[2 * e2 - 3];
+      const __bf16 h0 = static_cast<__bf16>(x0), h1 = static_cast<__bf16>(x1);
+      const float r0 = x0 - static_cast<float>(h0), r1 = x1 - static_cast<float>(h1);
+      const __bf16 m0 = static_cast<__bf16>(r0), m1 = static_cast<__bf16>(r1);
+      const float q0 = r0 - static_cast<float>(m0), q1 = r1 - static_cast<float>(m1);
+      o.h[blk][2 * e2] = h0;
+      o.h[blk][2 * e2 + 1] = h1;
+      o.m[blk][2 * e2] = m0;
+      o.m[blk][2 * e2 + 1] = m1;
+      o.l[blk][2 * e2] = static_cast<__bf16>(q0);
+      o.l[blk][2 * e2 + 1] = static_cast<__bf16>(q1);
+    }
+  };
+  auto mfma_slot = [&](auto ic, const GramOps& o) {
+    constexpr int i = decltype(ic)::value;
+    constexpr int t = i / 6, term = i % 6;
+    constexpr int ti = C::kTileI(t), tj = C::kTileJ(t);
+    if constexpr (term == 0) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.h[tj], acc[t], 0, 0, 0);
+    if constexpr (term == 1) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.m[tj], acc[t], 0, 0, 0);
+    if constexpr (term == 2) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.m[ti], o.h[tj], acc[t], 0, 0, 0);
+    if constexpr (term == 3) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.l[tj], acc[t], 0, 0, 0);
+    if constexpr (term == 4) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.l[ti], o.h[tj], acc[t], 0, 0, 0);
+    if constexpr (term == 5) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.m[ti], o.m[tj], acc[t], 0, 0, 0);
+  };
+
+  GramOps opA, opB;
+  if (nstage > 0) {
+#pragma unroll
+    for (int q = 0; q < C::LOADS; ++q) load_one(stage_k(0), q);
+#pragma unroll
+    for (int q = 0; q < C::LOADS; ++q) store_one(bufp(0), q);
+#pragma unroll
+    for (int q = 0; q < C::LOADS; ++q) load_one(stage_k(1), q);
+    __syncthreads();
+    static_for<0, 43>([&](auto pc) { prep_piece(pc, bufp(0), kg, opA); });
+  }
+
+  for (int s = 0; s < nstage; ++s) {
+    const float* b = bufp(s & 1);
+    float* bn = bufp((s + 1) & 1);
+    // phase A (past the last stage the store writes a copy of the last stage
+    // into the free buffer: nobody reads it)
+    static_for<0, 60>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      mfma_slot(ic, opA);
+      if constexpr (i < 43) prep_piece(ic, b, kg + 4, opB);
+      else if constexpr (i < 59) store_one(bn, i - 43);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __syncthreads();
+    // phase B
+    const int64_t k2 = stage_k(s + 2);
+    static_for<0, 60>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      mfma_slot(ic, opB);
+      if constexpr (i < 43) prep_piece(ic, bn, kg, opA);
+      else if constexpr (i < 59) load_one(k2, i - 43);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+
+  float* my = slab + (static_cast<int64_t>(blockIdx.x) * C::WK + kg) * T * 1024;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    float* o = my + t * 1024;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      o[row * 32 + r] = acc[t][reg];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) gram_pipe_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                                        float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  gram_body_pipe(X, n, d, ldx, slab, lds);
+}
+
+template <int NB, int WAVES, bool VEC, int STG = 0, int PF = 1, bool WM = false>
 __global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* __restrict__ X,
                                                                   const float* __restrict__ X2, int split, int n,
                                                                   int64_t d, int64_t ldx,
@@ -307,7 +576,7 @@ __global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* _
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int WT = GramCfg<NB, WAVES, STG>::WT;
   const int tg = (threadIdx.x >> 6) % WT;  // wave-uniform
-#define SRA_GB(TGV) gram_body<NB, WAVES, VEC, TGV, STG>(X, X2, split, n, d, ldx, shift, chunk, slab, lds)
+#define SRA_GB(TGV) gram_body<NB, WAVES, VEC, TGV, STG, PF, WM>(X, X2, split, n, d, ldx, shift, chunk, slab, lds)
   if (tg == 0) SRA_GB(0);
   if constexpr (WT > 1) if (tg == 1) SRA_GB(1);
   if constexpr (WT > 2) {
@@ -431,7 +700,7 @@ struct GramPair {
   int split, off_a, off_b, ldg, write_aa, write_bb;
 };
 
-template <int NB, int WAVES, int STG = 0>
+template <int NB, int WAVES, int STG = 0, int PF = 1, bool WM = false, bool PIPE = false>
 static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s,
                            const GramPair* pr = nullptr) {
   using C = GramCfg<NB, WAVES, STG>;
@@ -443,15 +712,23 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
   const float* shift = pr ? pr->shift : nullptr;
   const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(X2) & 15) == 0);
-  if (vec) {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true, STG>),
+  if constexpr (PIPE) {
+    static_assert(NB == 4 && WAVES == 4 && STG == 0, "pipelined Gram: N in (96, 128], four waves");
+    SRA_REQUIRE(pr == nullptr && n == 128 && vec && d % C::STAGE == 0, SRA_ERR_ARG,
+                "pipelined Gram needs N == 128, aligned rows and d %% %d == 0", C::STAGE);
+    const size_t lds2 = sizeof(float) * 2 * C::BUF;
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_pipe_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds2)));
+    hipLaunchKernelGGL(gram_pipe_kernel, dim3(nwg), dim3(256), lds2, s, X, n, d, ldx, slab);
+  } else if (vec) {
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true, STG, PF, WM>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true, STG>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split,
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, true, STG, PF, WM>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2, split,
                        n, d, ldx, shift, chunk, slab);
   } else {
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, false, STG>),
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, false, STG, PF, WM>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false, STG>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2,
+    hipLaunchKernelGGL((gram_partial_kernel<NB, WAVES, false, STG, PF, WM>), dim3(nwg), dim3(C::THREADS), lds, s, X, X2,
                        split, n, d, ldx, shift, chunk, slab);
   }
   int rc = launch_status("gram_partial_kernel");
@@ -476,8 +753,23 @@ static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double*
   // SRA_GRAM_STAGE64=1: 64-coordinate stages for N <= 128, half the LDS, two
   // workgroups per CU (A/B runs)
   static const int st64 = [] { const char* e = getenv("SRA_GRAM_STAGE64"); return e && *e ? atoi(e) : 0; }();
+  // SRA_GRAM_V (N <= 128, unpaired): 0 one register stage set + partial-sum
+  // means (two barriers per stage); 1 two sets in flight; 2 two sets + per-wave
+  // means (one barrier); 3 one set + per-wave means
+  static const int gv = [] { const char* e = getenv("SRA_GRAM_V"); return e && *e ? atoi(e) : 0; }();
   if constexpr (NB <= 4) {
     if (st64 == 1 && gram_waves(NB) == 4) return launch_gram_nbw<NB, 4, 64>(X, n, d, ldx, G, slab, s, pr);
+    if (pr == nullptr && gram_waves(NB) == 4) {
+      if (gv == 1) return launch_gram_nbw<NB, 4, 0, 2, false>(X, n, d, ldx, G, slab, s, pr);
+      if (gv == 2) return launch_gram_nbw<NB, 4, 0, 2, true>(X, n, d, ldx, G, slab, s, pr);
+      if (gv == 3) return launch_gram_nbw<NB, 4, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
+      if (gv == 4) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
+      if constexpr (NB == 4) {
+        const bool aligned = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+        if (gv == 5 && n == 128 && aligned && d % 128 == 0)
+          return launch_gram_nbw<4, 4, 0, 1, true, true>(X, n, d, ldx, G, slab, s, pr);
+      }
+    }
   }
   if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
   return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s, pr);

@@ -63,6 +63,25 @@ def test_gram_matches_fp64(n):
     np.testing.assert_allclose(got, d2, rtol=2e-5, atol=1e-9 * d2.max())
 
 
+@pytest.mark.parametrize("k", [1, 5, 257, 600])
+def test_gram_n128_whole_stages(k):
+    """N = 128 with d a multiple of the 128-coordinate stage: the software-
+    pipelined Gram (gram_pipe_kernel) when selected; workgroups with 0, 1, 2 and
+    3 stages; identical rows keep distance exactly 0."""
+    n, d = 128, 128 * k
+    x = make_rows(n, d, seed=900 + k, byz=8, identical_byz=True)
+    G = engine.gram(torch.from_numpy(x).cuda()).cpu().numpy()
+    xc = x.astype(np.float64)
+    xc -= xc.mean(axis=0)
+    gc = xc @ xc.T
+    d2 = np.maximum(np.diag(gc)[:, None] + np.diag(gc)[None, :] - 2 * gc, 0.0)
+    got = np.diag(G)[:, None] + np.diag(G)[None, :] - 2 * G
+    np.testing.assert_allclose(got, d2, rtol=2e-5, atol=1e-9 * d2.max())
+    for i in range(8):
+        for j in range(8):
+            assert got[i, j] == 0.0
+
+
 def test_identical_rows_zero_distance_and_unaligned():
     x = make_rows(40, 2051, seed=5, byz=8, identical_byz=True)
     X = torch.from_numpy(x).cuda()
