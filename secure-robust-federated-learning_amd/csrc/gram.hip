@@ -137,6 +137,28 @@ __device__ __forceinline__ float sum_lanes_32(float x) {
   return x;
 }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// the exact three-way split of two values, packed: one v_cvt_pk_bf16_f32 per
+// level, the bf16 -> fp32 widening by shift / mask (the same bits as split3)
+__device__ __forceinline__ void split3_pair(float x0, float x1, uint32_t& hb, uint32_t& mb, uint32_t& lb) {
+  hb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
+  const float r0 = x0 - __builtin_bit_cast(float, hb << 16);
+  const float r1 = x1 - __builtin_bit_cast(float, hb & 0xffff0000u);
+  mb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
+  const float q0 = r0 - __builtin_bit_cast(float, mb << 16);
+  const float q1 = r1 - __builtin_bit_cast(float, mb & 0xffff0000u);
+  lb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){q0, q1}, bf16x2));
+}
+
+__device__ __forceinline__ void set_pair(bf16x8& v, int e2, uint32_t bits) {
+  u32x4 u = __builtin_bit_cast(u32x4, v);
+  u[e2] = bits;
+  v = __builtin_bit_cast(bf16x8, u);
+}
+
 template <int V>
 struct IC {
   static constexpr int value = V;
@@ -411,6 +433,7 @@ struct GramOps {
 // d a multiple of the 128-coordinate stage, so every load is a full, guard-free
 // float4 and the loop body is one basic block (no branch for sched_barrier to
 // stop at); past the last stage the loads re-read the last stage (discarded).
+template <int LM>
 __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
                                                float* __restrict__ slab, float* lds) {
   using C = GramCfg<4, 4, 0>;
@@ -458,10 +481,12 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
       const float* rp = b + (32 * p + r) * C::ROWPAD + col;
       raw0[p] = *reinterpret_cast<const f32x4*>(rp);
       raw1[p] = *reinterpret_cast<const f32x4*>(rp + 4);
-    } else if constexpr (p == 4) {
-      mu0 = ((raw0[0] + raw0[1]) + raw0[2]) + raw0[3];
+    } else if constexpr (p == 4) {   // scalar adds: packed f32 VALU is slow beside MFMAs
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mu0[e] = ((raw0[0][e] + raw0[1][e]) + raw0[2][e]) + raw0[3][e];
     } else if constexpr (p == 5) {
-      mu1 = ((raw1[0] + raw1[1]) + raw1[2]) + raw1[3];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mu1[e] = ((raw1[0][e] + raw1[1][e]) + raw1[2][e]) + raw1[3][e];
     } else if constexpr (p < 26) {
       // butterfly: level-major, two of the eight values per piece
       constexpr int q = p - 6;          // 0..19
@@ -481,24 +506,22 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
         if (vv < 4) mu0[vv] = x; else mu1[vv - 4] = x;
       }
     } else if constexpr (p == 26) {
-      mu0 *= inv_n;
-      mu1 *= inv_n;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mu0[e] = mu0[e] * inv_n;
+        mu1[e] = mu1[e] * inv_n;
+      }
     } else if constexpr (p < 43) {
       // centre + split one element pair of one block
       constexpr int blk = (p - 27) / 4;
       constexpr int e2 = (p - 27) % 4;
       float x0 = e2 < 2 ? raw0[blk][2 * e2] - mu0[2 * e2] : raw1[blk][2 * e2 - 4] - mu1[2 * e2 - 4];
       float x1 = e2 < 2 ? raw0[blk][2 * e2 + 1] - mu0[2 * e2 + 1] : raw1[blk][2 * e2 - 3] - mu1[2 * e2 - 3];
-      const __bf16 h0 = static_cast<__bf16>(x0), h1 = static_cast<__bf16>(x1);
-      const float r0 = x0 - static_cast<float>(h0), r1 = x1 - static_cast<float>(h1);
-      const __bf16 m0 = static_cast<__bf16>(r0), m1 = static_cast<__bf16>(r1);
-      const float q0 = r0 - static_cast<float>(m0), q1 = r1 - static_cast<float>(m1);
-      o.h[blk][2 * e2] = h0;
-      o.h[blk][2 * e2 + 1] = h1;
-      o.m[blk][2 * e2] = m0;
-      o.m[blk][2 * e2 + 1] = m1;
-      o.l[blk][2 * e2] = static_cast<__bf16>(q0);
-      o.l[blk][2 * e2 + 1] = static_cast<__bf16>(q1);
+      uint32_t hb, mb, lb;
+      split3_pair(x0, x1, hb, mb, lb);
+      set_pair(o.h[blk], e2, hb);
+      set_pair(o.m[blk], e2, mb);
+      set_pair(o.l[blk], e2, lb);
     }
   };
   auto mfma_slot = [&](auto ic, const GramOps& o) {
@@ -530,21 +553,25 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
     float* bn = bufp((s + 1) & 1);
     // phase A (past the last stage the store writes a copy of the last stage
     // into the free buffer: nobody reads it)
+    const int64_t k2 = stage_k(s + 2);
     static_for<0, 60>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       mfma_slot(ic, opA);
-      if constexpr (i < 43) prep_piece(ic, b, kg + 4, opB);
-      else if constexpr (i < 59) store_one(bn, i - 43);
+      if constexpr (i < 43) {
+        prep_piece(ic, b, kg + 4, opB);
+      } else if constexpr (i < 59) {
+        store_one(bn, i - 43);
+        if constexpr (LM == 1) load_one(k2, i - 43);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
     __syncthreads();
     // phase B
-    const int64_t k2 = stage_k(s + 2);
     static_for<0, 60>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       mfma_slot(ic, opB);
       if constexpr (i < 43) prep_piece(ic, bn, kg, opA);
-      else if constexpr (i < 59) load_one(k2, i - 43);
+      else if constexpr (i < 59 && LM == 0) load_one(k2, i - 43);
       __builtin_amdgcn_sched_barrier(0);
     });
   }
@@ -561,10 +588,14 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
   }
 }
 
+// LM: where the next-but-one stage's loads are issued (0: phase B, 1: phase A
+// right behind the stores, 1.5 phases ahead of their use; 2: not at all --
+// timing experiment only, the result is wrong)
+template <int LM>
 __global__ void __launch_bounds__(256) gram_pipe_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
                                                         float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  gram_body_pipe(X, n, d, ldx, slab, lds);
+  gram_body_pipe<LM>(X, n, d, ldx, slab, lds);
 }
 
 template <int NB, int WAVES, bool VEC, int STG = 0, int PF = 1, bool WM = false>
@@ -717,9 +748,15 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
     SRA_REQUIRE(pr == nullptr && n == 128 && vec && d % C::STAGE == 0, SRA_ERR_ARG,
                 "pipelined Gram needs N == 128, aligned rows and d %% %d == 0", C::STAGE);
     const size_t lds2 = sizeof(float) * 2 * C::BUF;
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_pipe_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds2)));
-    hipLaunchKernelGGL(gram_pipe_kernel, dim3(nwg), dim3(256), lds2, s, X, n, d, ldx, slab);
+    auto go = [&](auto kern) {
+      SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds2)));
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds2, s, X, n, d, ldx, slab);
+      return SRA_OK;
+    };
+    const int lm = PF;   // PIPE reuses PF as the load placement
+    int rc0 = lm == 1 ? go(&gram_pipe_kernel<1>) : (lm == 2 ? go(&gram_pipe_kernel<2>) : go(&gram_pipe_kernel<0>));
+    if (rc0) return rc0;
   } else if (vec) {
     SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true, STG, PF, WM>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
@@ -766,8 +803,11 @@ static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double*
       if (gv == 4) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
       if constexpr (NB == 4) {
         const bool aligned = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-        if (gv == 5 && n == 128 && aligned && d % 128 == 0)
-          return launch_gram_nbw<4, 4, 0, 1, true, true>(X, n, d, ldx, G, slab, s, pr);
+        if (gv >= 5 && gv <= 7 && n == 128 && aligned && d % 128 == 0) {
+          if (gv == 6) return launch_gram_nbw<4, 4, 0, 1, true, true>(X, n, d, ldx, G, slab, s, pr);
+          if (gv == 7) return launch_gram_nbw<4, 4, 0, 2, true, true>(X, n, d, ldx, G, slab, s, pr);
+          return launch_gram_nbw<4, 4, 0, 0, true, true>(X, n, d, ldx, G, slab, s, pr);
+        }
       }
     }
   }
