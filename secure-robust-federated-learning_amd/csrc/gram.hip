@@ -790,25 +790,30 @@ static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double*
   // SRA_GRAM_STAGE64=1: 64-coordinate stages for N <= 128, half the LDS, two
   // workgroups per CU (A/B runs)
   static const int st64 = [] { const char* e = getenv("SRA_GRAM_STAGE64"); return e && *e ? atoi(e) : 0; }();
-  // SRA_GRAM_V (N <= 128, unpaired): 0 one register stage set + partial-sum
-  // means (two barriers per stage); 1 two sets in flight; 2 two sets + per-wave
-  // means (one barrier); 3 one set + per-wave means
-  static const int gv = [] { const char* e = getenv("SRA_GRAM_V"); return e && *e ? atoi(e) : 0; }();
+  // SRA_GRAM_V (N <= 128, unpaired; A/B runs, DESIGN k2): default -1 = the
+  // pipelined kernel with phase-A loads where it applies (N == 128, aligned
+  // rows, d % 128 == 0), per-wave means elsewhere; 0 round 2's kernel (one
+  // register stage set, partial-sum means, two barriers per stage); 1 two
+  // stage sets in flight; 2 two sets + per-wave means; 3 per-wave means;
+  // 4 per-wave means on eight waves; 5 / 6 pipelined with phase-B / phase-A
+  // loads; 7 pipelined without stage loads (timing only: WRONG results)
+  static const int gv = [] { const char* e = getenv("SRA_GRAM_V"); return e && *e ? atoi(e) : -1; }();
   if constexpr (NB <= 4) {
     if (st64 == 1 && gram_waves(NB) == 4) return launch_gram_nbw<NB, 4, 64>(X, n, d, ldx, G, slab, s, pr);
     if (pr == nullptr && gram_waves(NB) == 4) {
-      if (gv == 1) return launch_gram_nbw<NB, 4, 0, 2, false>(X, n, d, ldx, G, slab, s, pr);
-      if (gv == 2) return launch_gram_nbw<NB, 4, 0, 2, true>(X, n, d, ldx, G, slab, s, pr);
-      if (gv == 3) return launch_gram_nbw<NB, 4, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
-      if (gv == 4) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
       if constexpr (NB == 4) {
         const bool aligned = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-        if (gv >= 5 && gv <= 7 && n == 128 && aligned && d % 128 == 0) {
-          if (gv == 6) return launch_gram_nbw<4, 4, 0, 1, true, true>(X, n, d, ldx, G, slab, s, pr);
+        if ((gv == -1 || (gv >= 5 && gv <= 7)) && n == 128 && aligned && d % 128 == 0) {
+          if (gv == 5) return launch_gram_nbw<4, 4, 0, 0, true, true>(X, n, d, ldx, G, slab, s, pr);
           if (gv == 7) return launch_gram_nbw<4, 4, 0, 2, true, true>(X, n, d, ldx, G, slab, s, pr);
-          return launch_gram_nbw<4, 4, 0, 0, true, true>(X, n, d, ldx, G, slab, s, pr);
+          return launch_gram_nbw<4, 4, 0, 1, true, true>(X, n, d, ldx, G, slab, s, pr);
         }
       }
+      if (gv == 0) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
+      if (gv == 1) return launch_gram_nbw<NB, 4, 0, 2, false>(X, n, d, ldx, G, slab, s, pr);
+      if (gv == 2) return launch_gram_nbw<NB, 4, 0, 2, true>(X, n, d, ldx, G, slab, s, pr);
+      if (gv == 4) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
+      return launch_gram_nbw<NB, 4, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
     }
   }
   if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
