@@ -41,13 +41,11 @@
 // 32x32x16 per tile and k-step, 10 tiles) is ~0.5 ms per 1e7 coordinates at
 // the 2.5 PF bf16 peak, below the ~0.8 ms of HBM time.
 #include "sra_common.hpp"
+#include "gram_common.hpp"
 
 #include <cstdlib>
 
 namespace sra {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // exact three-way bf16 split of 8 fp32 values: x = h + m + l
 __device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
@@ -63,47 +61,6 @@ __device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, bf16x8& h
     l[e] = static_cast<__bf16>(r2);
   }
 }
-
-template <int NB, int WAVES = 4, int STG = 0>
-struct GramCfg {
-  static constexpr int NP = 32 * NB;
-  static constexpr int THREADS = 64 * WAVES;
-  static constexpr int STAGE = STG ? STG : (NB <= 4 ? 128 : 64);  // coordinates per stage
-  static constexpr int ROWPAD = STAGE + 4;                       // LDS row stride (floats)
-  static constexpr int T = NB * (NB + 1) / 2;                    // upper-triangle tiles
-  // tile groups: 4 waves -> keep <= 176 accumulators per wave; 8 waves (two
-  // per SIMD) -> <= 128 so that a wave fits in 256 registers
-  static constexpr int WT = WAVES == 4 ? (NB <= 4 ? 1 : (NB <= 6 ? 2 : 4))
-                                       : (NB <= 3 ? 1 : (NB <= 5 ? 2 : (NB <= 7 ? 4 : 8)));
-  static constexpr int WK = WAVES / WT;                          // k groups
-  static constexpr int TPW = (T + WT - 1) / WT;                  // tiles per wave (max)
-  static constexpr int KSTEPS = STAGE / 16;                      // 16-coordinate k-steps per stage
-  static constexpr int KPW = KSTEPS / WK;                        // k-steps per wave per stage
-  static constexpr int C4 = STAGE / 4;                           // float4 columns per row
-  static constexpr int RSTEP = THREADS / C4;                     // rows covered per load sweep
-  static constexpr int LOADS = NP / RSTEP > 0 ? NP / RSTEP : 1;  // float4 per thread per stage
-  static constexpr int kTileI(int t) {
-    int c = 0;
-    for (int i = 0; i < NB; ++i)
-      for (int j = i; j < NB; ++j) {
-        if (c == t) return i;
-        ++c;
-      }
-    return 0;
-  }
-  static constexpr int kTileJ(int t) {
-    int c = 0;
-    for (int i = 0; i < NB; ++i)
-      for (int j = i; j < NB; ++j) {
-        if (c == t) return j;
-        ++c;
-      }
-    return 0;
-  }
-  static constexpr int BUF = NP * ROWPAD;                        // floats per stage buffer
-  static constexpr int PART = WAVES * STAGE;                     // per-wave column partials
-  static constexpr int lds_floats = 2 * BUF + PART + 2 * STAGE;  // stage buffers, partials, means
-};
 
 template <int NB, int WAVES, int STG = 0>
 int gram_slab_floats_t(int64_t num_wg) {
@@ -136,33 +93,6 @@ __device__ __forceinline__ float sum_lanes_32(float x) {
   x += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), 0x401f));
   return x;
 }
-
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// the exact three-way split of two values, packed: one v_cvt_pk_bf16_f32 per
-// level, the bf16 -> fp32 widening by shift / mask (the same bits as split3)
-__device__ __forceinline__ void split3_pair(float x0, float x1, uint32_t& hb, uint32_t& mb, uint32_t& lb) {
-  hb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
-  const float r0 = x0 - __builtin_bit_cast(float, hb << 16);
-  const float r1 = x1 - __builtin_bit_cast(float, hb & 0xffff0000u);
-  mb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
-  const float q0 = r0 - __builtin_bit_cast(float, mb << 16);
-  const float q1 = r1 - __builtin_bit_cast(float, mb & 0xffff0000u);
-  lb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){q0, q1}, bf16x2));
-}
-
-__device__ __forceinline__ void set_pair(bf16x8& v, int e2, uint32_t bits) {
-  u32x4 u = __builtin_bit_cast(u32x4, v);
-  u[e2] = bits;
-  v = __builtin_bit_cast(bf16x8, u);
-}
-
-template <int V>
-struct IC {
-  static constexpr int value = V;
-};
 
 // PF: register stage sets in flight (2: the loads of stage s + 3 are issued
 // while stage s computes, two stages of MFMA work to cover HBM latency).
@@ -401,203 +331,6 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
   }
 }
 
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(IC<I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// Software-pipelined Gram for 96 < N <= 128 (NB = 4, four waves, the C3
-// shape).  Same arithmetic as gram_body<4, 4, VEC, 0, 1, true> (per-wave means
-// from a fixed butterfly, the exact three-way split, six bf16 MFMAs per tile
-// and k-step, tiles accumulated in the same k order), scheduled so that the
-// MFMA pipe is never left idle while the wave does its VALU work: each of the
-// 60 MFMAs of a k-step is followed by one small piece of the NEXT k-step's
-// preparation (its LDS reads, the column sums and butterfly, the centring and
-// split of one element pair) or of the stage traffic (one ds_write_b128 of the
-// next stage, one global load of the stage after), pinned in place by
-// sched_barrier.  Stage s:
-//   phase A: MFMA(k-step g0 of s) | prepare g1 of s (LDS s)   | store s+1 -> LDS
-//   barrier
-//   phase B: MFMA(k-step g1 of s) | prepare g0 of s+1 (LDS s+1) | load s+2
-// One barrier per stage: buffer s&1 is last read in phase A of stage s and next
-// written in phase A of stage s+1; buffer (s+1)&1 is written in phase A of s and
-// first read after the barrier.
-struct GramOps {
-  bf16x8 h[4], m[4], l[4];
-};
-
-// Host contract (launch_gram_nbw<..., PIPE>): N == 128, 16-byte aligned rows,
-// d a multiple of the 128-coordinate stage, so every load is a full, guard-free
-// float4 and the loop body is one basic block (no branch for sched_barrier to
-// stop at); past the last stage the loads re-read the last stage (discarded).
-template <int LM>
-__device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
-                                               float* __restrict__ slab, float* lds) {
-  using C = GramCfg<4, 4, 0>;
-  constexpr int STAGE = C::STAGE;   // 128
-  constexpr int T = C::T;           // 10
-  static_assert(C::WK == 4 && C::KPW == 2 && C::LOADS == 16 && T == 10, "pipe layout");
-  auto bufp = [&](int which) { return lds + which * C::BUF; };
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int kg = tid >> 6;
-  const int64_t ntiles = d / STAGE;
-  const int nstage = blockIdx.x < ntiles ? static_cast<int>(cdiv(ntiles - blockIdx.x, gridDim.x)) : 0;
-  const float inv_n = 1.0f / static_cast<float>(n);
-  const int r = lane & 31;
-  const int h = lane >> 5;
-
-  f32x16 acc[T];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-
-  f32x4 stg[C::LOADS];
-  const int c4 = tid % C::C4;
-  const int row0 = tid / C::C4;
-  const uint32_t lane_off = static_cast<uint32_t>((static_cast<int64_t>(row0) * ldx + 4 * c4) * 4);
-  auto stage_k = [&](int s) {
-    return (static_cast<int64_t>(s < nstage ? s : nstage - 1) * gridDim.x + blockIdx.x) * STAGE;
-  };
-  auto load_one = [&](int64_t kb, int q) {
-    const char* bq = reinterpret_cast<const char*>(X + static_cast<int64_t>(C::RSTEP * q) * ldx + kb);
-    stg[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(bq + lane_off));
-  };
-  auto store_one = [&](float* b, int q) {
-    *reinterpret_cast<f32x4*>(b + (row0 + C::RSTEP * q) * C::ROWPAD + 4 * c4) = stg[q];
-  };
-
-  // preparation of one k-step, split in 43 pieces
-  f32x4 raw0[4], raw1[4], mu0, mu1;
-  auto prep_piece = [&](auto pc, const float* b, int g, GramOps& o) {
-    constexpr int p = decltype(pc)::value;
-    const int col = 16 * g + 8 * h;
-    if constexpr (p < 4) {
-      const float* rp = b + (32 * p + r) * C::ROWPAD + col;
-      raw0[p] = *reinterpret_cast<const f32x4*>(rp);
-      raw1[p] = *reinterpret_cast<const f32x4*>(rp + 4);
-    } else if constexpr (p == 4) {   // scalar adds: packed f32 VALU is slow beside MFMAs
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mu0[e] = ((raw0[0][e] + raw0[1][e]) + raw0[2][e]) + raw0[3][e];
-    } else if constexpr (p == 5) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mu1[e] = ((raw1[0][e] + raw1[1][e]) + raw1[2][e]) + raw1[3][e];
-    } else if constexpr (p < 26) {
-      // butterfly: level-major, two of the eight values per piece
-      constexpr int q = p - 6;          // 0..19
-      constexpr int lvl = q / 4;        // 0..4
-      constexpr int v0 = 2 * (q % 4);   // values v0, v0 + 1 of (mu0, mu1)
-#pragma unroll
-      for (int vv = v0; vv < v0 + 2; ++vv) {
-        float x = vv < 4 ? mu0[vv] : mu1[vv - 4];
-        int xi = __builtin_bit_cast(int, x);
-        int yi;
-        if constexpr (lvl == 0) yi = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
-        else if constexpr (lvl == 1) yi = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
-        else if constexpr (lvl == 2) yi = __builtin_amdgcn_ds_swizzle(xi, 0x101f);
-        else if constexpr (lvl == 3) yi = __builtin_amdgcn_ds_swizzle(xi, 0x201f);
-        else yi = __builtin_amdgcn_ds_swizzle(xi, 0x401f);
-        x += __builtin_bit_cast(float, yi);
-        if (vv < 4) mu0[vv] = x; else mu1[vv - 4] = x;
-      }
-    } else if constexpr (p == 26) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        mu0[e] = mu0[e] * inv_n;
-        mu1[e] = mu1[e] * inv_n;
-      }
-    } else if constexpr (p < 43) {
-      // centre + split one element pair of one block
-      constexpr int blk = (p - 27) / 4;
-      constexpr int e2 = (p - 27) % 4;
-      float x0 = e2 < 2 ? raw0[blk][2 * e2] - mu0[2 * e2] : raw1[blk][2 * e2 - 4] - mu1[2 * e2 - 4];
-      float x1 = e2 < 2 ? raw0[blk][2 * e2 + 1] - mu0[2 * e2 + 1] : raw1[blk][2 * e2 - 3] - mu1[2 * e2 - 3];
-      uint32_t hb, mb, lb;
-      split3_pair(x0, x1, hb, mb, lb);
-      set_pair(o.h[blk], e2, hb);
-      set_pair(o.m[blk], e2, mb);
-      set_pair(o.l[blk], e2, lb);
-    }
-  };
-  auto mfma_slot = [&](auto ic, const GramOps& o) {
-    constexpr int i = decltype(ic)::value;
-    constexpr int t = i / 6, term = i % 6;
-    constexpr int ti = C::kTileI(t), tj = C::kTileJ(t);
-    if constexpr (term == 0) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.h[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 1) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.m[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 2) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.m[ti], o.h[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 3) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.l[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 4) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.l[ti], o.h[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 5) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.m[ti], o.m[tj], acc[t], 0, 0, 0);
-  };
-
-  GramOps opA, opB;
-  if (nstage > 0) {
-#pragma unroll
-    for (int q = 0; q < C::LOADS; ++q) load_one(stage_k(0), q);
-#pragma unroll
-    for (int q = 0; q < C::LOADS; ++q) store_one(bufp(0), q);
-#pragma unroll
-    for (int q = 0; q < C::LOADS; ++q) load_one(stage_k(1), q);
-    __syncthreads();
-    static_for<0, 43>([&](auto pc) { prep_piece(pc, bufp(0), kg, opA); });
-  }
-
-  for (int s = 0; s < nstage; ++s) {
-    const float* b = bufp(s & 1);
-    float* bn = bufp((s + 1) & 1);
-    // phase A (past the last stage the store writes a copy of the last stage
-    // into the free buffer: nobody reads it)
-    const int64_t k2 = stage_k(s + 2);
-    static_for<0, 60>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      mfma_slot(ic, opA);
-      if constexpr (i < 43) {
-        prep_piece(ic, b, kg + 4, opB);
-      } else if constexpr (i < 59) {
-        store_one(bn, i - 43);
-        if constexpr (LM == 1) load_one(k2, i - 43);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    __syncthreads();
-    // phase B
-    static_for<0, 60>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      mfma_slot(ic, opB);
-      if constexpr (i < 43) prep_piece(ic, bn, kg, opA);
-      else if constexpr (i < 59 && LM == 0) load_one(k2, i - 43);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-
-  float* my = slab + (static_cast<int64_t>(blockIdx.x) * C::WK + kg) * T * 1024;
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    float* o = my + t * 1024;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      o[row * 32 + r] = acc[t][reg];
-    }
-  }
-}
-
-// LM: where the next-but-one stage's loads are issued (0: phase B, 1: phase A
-// right behind the stores, 1.5 phases ahead of their use; 2: not at all --
-// timing experiment only, the result is wrong)
-template <int LM>
-__global__ void __launch_bounds__(256) gram_pipe_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
-                                                        float* __restrict__ slab) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  gram_body_pipe<LM>(X, n, d, ldx, slab, lds);
-}
-
 template <int NB, int WAVES, bool VEC, int STG = 0, int PF = 1, bool WM = false>
 __global__ void __launch_bounds__(64 * WAVES) gram_partial_kernel(const float* __restrict__ X,
                                                                   const float* __restrict__ X2, int split, int n,
@@ -747,15 +480,7 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
     static_assert(NB == 4 && WAVES == 4 && STG == 0, "pipelined Gram: N in (96, 128], four waves");
     SRA_REQUIRE(pr == nullptr && n == 128 && vec && d % C::STAGE == 0, SRA_ERR_ARG,
                 "pipelined Gram needs N == 128, aligned rows and d %% %d == 0", C::STAGE);
-    const size_t lds2 = sizeof(float) * 2 * C::BUF;
-    auto go = [&](auto kern) {
-      SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(lds2)));
-      hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds2, s, X, n, d, ldx, slab);
-      return SRA_OK;
-    };
-    const int lm = PF;   // PIPE reuses PF as the load placement
-    int rc0 = lm == 1 ? go(&gram_pipe_kernel<1>) : (lm == 2 ? go(&gram_pipe_kernel<2>) : go(&gram_pipe_kernel<0>));
+    const int rc0 = launch_gram_pipe(X, n, d, ldx, slab, nwg, PF, s);
     if (rc0) return rc0;
   } else if (vec) {
     SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true, STG, PF, WM>),
