@@ -310,9 +310,13 @@ __device__ __forceinline__ void gram_body(const float* __restrict__ X, const flo
       }
     }
   };
-  for (int s = 0; s < nstage; s += 2) {
-    step(s, IC<0>{});
-    if (s + 1 < nstage) step(s + 1, IC<1>{});
+  if constexpr (PF == 1) {
+    for (int s = 0; s < nstage; ++s) step(s, IC<0>{});   // one body: the I-cache holds it
+  } else {
+    for (int s = 0; s < nstage; s += 2) {
+      step(s, IC<0>{});
+      if (s + 1 < nstage) step(s + 1, IC<1>{});
+    }
   }
 
   // ---- partial tiles -> slab[wg][kg][tile][32 x 32] (row-major) ----
