@@ -108,7 +108,6 @@ __global__ void __launch_bounds__(256, 3) select_dist_rows_kernel(const float* _
     const int li = 64 * q + static_cast<int>(lane);
     rl[q] = rows[li < n_arg ? li : n_arg - 1];
   }
-  __shared__ float aggs[4][64];
   __shared__ float dl[4][32][68];   // row stride 68 words: the transposed b128 reads spread over the banks
   __shared__ float wsum[4][P];
   float bs = 0.f;

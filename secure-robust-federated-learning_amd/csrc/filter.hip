@@ -1081,9 +1081,9 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
 // the residual decay, so a check never lands after a ghost copy of the top
 // Ritz value has formed (~15-20 steps after convergence).  A chunk that has
 // not converged after MMAX steps, or whose residual grows between checks (a
-// ghost), is listed for filter_solve_kernel and redone from its first iteration.
+// ghost) after a dense-check retry, takes a third, re-orthogonalising attempt
+// in the same kernel (classical Gram-Schmidt + DGKS against the stored basis).
 constexpr int MMAX = 128;          // plain Lanczos steps per eigenproblem (two lane slots of the check)
-constexpr int TW = 2 * MMAX + 4;   // per-wave T record: (alpha_q, beta^2_{q-1}) interleaved, then z
 constexpr int kMaxAdvance = 8;     // checks at most this far apart (a ghost forms ~15-20 steps past convergence)
 constexpr double kAccept = 2.5e-16;  // plain Lanczos: accept the Ritz pair at residual <= kAccept * lambda
 
@@ -1850,7 +1850,6 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         double nrm2 = o[0];
         double qprev = 0.0, theta_lb = -1e300, hint = -1.0;
         double res_best = 1e300, lam_best = 0.0;
-        int m_best = 0;
         tscale = 0.0;
         // incremental Gershgorin bounds of T: rows 0 .. j-2 final, plus row j-1
         double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
@@ -1902,7 +1901,6 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
                 m_pre = m_last;
                 res_best = res;
                 lam_best = lm;
-                m_best = m;
                 zbest = zcur;
                 zcur ^= 1;
               }
