@@ -548,6 +548,8 @@ static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double*
     }
   }
   if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
+  // SRA_GRAM_V=8 (A/B): per-wave means on the eight-wave kernels too (N > 128, unpaired)
+  if (gv == 8 && pr == nullptr) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
   return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s, pr);
 }
 
