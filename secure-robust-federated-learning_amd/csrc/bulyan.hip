@@ -1388,8 +1388,8 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
       (reinterpret_cast<uintptr_t>(bpart) + round_partial_bytes(n, d) + 255) & ~static_cast<uintptr_t>(255));
   int* cur = rows_a;
   int* nxt = rows_b;
-  // SRA_BULYAN_MEDIAN_1READ=0 keeps the fused two-read rounds (A/B)
-  static const int one_read = [] { const char* e = getenv("SRA_BULYAN_MEDIAN_1READ"); return e && *e ? atoi(e) : 1; }();
+  // SRA_BULYAN_MEDIAN_1READ=1 takes the one-read median rounds (A/B against the fused two-read rounds)
+  static const int one_read = [] { const char* e = getenv("SRA_BULYAN_MEDIAN_1READ"); return e && *e ? atoi(e) : 0; }();
   if (mode == kBulyanMedian && !dba && n <= 128 && one_read) {
     f32x4* cand = reinterpret_cast<f32x4*>(
         (reinterpret_cast<uintptr_t>(dist + n) + 255) & ~static_cast<uintptr_t>(255));

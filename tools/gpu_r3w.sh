@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/r3w
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_bulyan.py tests/test_gpu_c3_bulyan.py tests/test_gpu_dba.py tests/test_gpu_shard.py > "$OUT/pytest.log" 2>&1
+SRA_BULYAN_MEDIAN_1READ=1 timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_bulyan.py tests/test_gpu_c3_bulyan.py tests/test_gpu_dba.py tests/test_gpu_shard.py > "$OUT/pytest.log" 2>&1
 rc=$?
 echo "pytest: $(grep -E "passed|failed" "$OUT/pytest.log" | tail -1)"
 [[ $rc -ne 0 ]] && { grep -E "FAILED|Error|assert" "$OUT/pytest.log" | head -20; exit $rc; }
