@@ -6,13 +6,13 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmcw
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-W="filterl2|--agg filterl2 --d 1e7
+W="${PMCW_LIST:-filterl2|--agg filterl2 --d 1e7
 ex_noregret|--agg ex_noregret --d 1e7
 mom_filterl2|--agg mom_filterl2 --clients 512 --d 1.25e7
 mom_ex_noregret|--agg mom_ex_noregret --clients 512 --d 1.25e7
 bulyankrum|--agg bulyankrum --d 1e7
 bulyantrimmedmean|--agg bulyantrimmedmean --d 1e7
-mom_krum|--agg mom_krum --clients 512 --d 1.25e7"
+mom_krum|--agg mom_krum --clients 512 --d 1.25e7}"
 while IFS='|' read -r name args; do
   timeout -k 10 300 python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --no-host $args > "$OUT/$name.log" 2>&1 \
     || { echo "bench $name failed rc=$?"; tail -5 "$OUT/$name.log"; exit 1; }
