@@ -93,7 +93,7 @@ def _device_rows(n, d, byz, seed):
     return X
 
 
-def _fullsize(X, mode, nsample=24, seed=0):
+def _fullsize(X, mode, nsample=48, seed=0):
     out, tr = engine.filter_trace(X, mode, SIM["eps"], SIM["sigma"], SIM["expansion"], SIM["itv"])
     n, d = X.shape
     nch = -(-d // SIM["itv"])
