@@ -1,6 +1,9 @@
 #!/bin/bash
 # Round 3, session u: same-box A/B of the session-start library (tools/ab) vs
 # the current one on the Krum family (mom_krum's N > 128 Gram in particular).
+# (tools/ab/libsra_r3start.so was built from commit 1405ea2: git worktree add /tmp/oldtree 1405ea2 &&
+#  make -C /tmp/oldtree/secure-robust-federated-learning_amd/csrc OUT=$PWD/tools/ab/libsra_r3start.so BUILD=/tmp/oldbuild;
+#  not kept in the tree)
 set -u
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/r3u
