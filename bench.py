@@ -26,19 +26,26 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
+import torch  # importing torch does not initialise the GPU; libsra is loaded in main()
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-import srfl_loader  # noqa: E402
+engine = shard = None   # srfl_amd modules, bound by _load_engine() once this process is a bench rank
 
-srfl = srfl_loader.load()
-from srfl_amd import engine, shard  # noqa: E402
+
+def _load_engine():
+    global engine, shard
+    import srfl_loader
+    srfl_loader.load()
+    from srfl_amd import engine as _e, shard as _s
+    engine, shard = _e, _s
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -62,7 +69,77 @@ def parse():
                          "overlapped with the aggregation of block k+1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC (written by tools/pmc_traffic.py)")
+    ap.add_argument("--byzantine", type=int, default=20,
+                    help="f Byzantine rows of the synthetic input (SURVEY.md §8(d)); 0 = benign only")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: every rank joins a gloo group, prints its rank / world size and exits "
+                         "(no GPU use); exercises the --gpus launcher on CPU")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def ranks_or_launch(a):
+    """--gpus N is honoured or the run fails: without WORLD_SIZE in the
+    environment and N > 1, start N ranks as ONE child process
+    (python -m torch.distributed.run, rendezvous on 127.0.0.1) and return its
+    exit code -- this happens before anything touches the GPU, and the parent
+    never execs; with WORLD_SIZE set it must equal N.  Returns None when this
+    process is a rank that should run the bench."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if a.gpus <= 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.call(cmd)
+    if int(env_world) != a.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d: launch one rank per GPU with --gpus equal to the world size"
+              % (env_world, a.gpus), file=sys.stderr, flush=True)
+        return 2
+    return None
+
+
+def launch_check(a):
+    """--launch-check: one gloo collective over the ranks the launcher started."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([1.0])
+    if world > 1:
+        dist.all_reduce(t)
+        world = dist.get_world_size()
+    print(json.dumps({"rank": rank, "world_size": world, "ranks_seen": int(t.item()), "gpus": a.gpus}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def synthetic_rows(n, d, byz, seed, device):
+    """SURVEY.md §8(d) synthetic updates, generated on the device: 0.01 N(0,1)
+    per client plus a shared 0.001 N(0,1) drift; rows < byz Byzantine at -10x
+    the benign mean plus 0.001 N(0,1) noise (the generator of the full-size
+    filter / Krum / Bulyan parity tests, tests/test_gpu_filters.py)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    X = torch.empty((n, d), dtype=torch.float32, device=device)
+    cols = max(1, int(1e9 // (8 * max(n, 1))))        # fp64 column-block of <= 1 GB for the benign mean
+    drift = torch.empty(min(d, cols), dtype=torch.float32, device=device)
+    for j0 in range(0, d, cols):
+        j1 = min(d, j0 + cols)
+        dv = drift[:j1 - j0].normal_(0.0, 0.001, generator=g)
+        blk = X[:, j0:j1]
+        blk.normal_(0.0, 0.01, generator=g).add_(dv)
+        if byz:
+            mean = blk[byz:].double().mean(0)
+            blk[:byz] = (-10.0 * mean).float()[None, :] + 0.001 * torch.randn(byz, j1 - j0, device=device,
+                                                                                 generator=g)
+    return X
 
 
 def _krum_step(X, out):
@@ -77,7 +154,7 @@ def _mom_krum_step(X, out):
 
 def _bulyan_step(mode):
     def step(X, out):
-        out.copy_(engine.bulyan(X, 20, mode))
+        out.copy_(engine.bulyan(X, 20, mode, check=False))
     return step
 
 
@@ -87,8 +164,9 @@ FILTER_ARGS = dict(eps=0.2, sigma=1e-5, expansion=20, itv=1000)
 MOM_DELTA = 2.718281828459045 ** -26
 
 
-def _filter_step(fn, mom=False):
+def _filter_step(name, mom=False):
     def step(X, out):
+        fn = getattr(engine, name)
         if mom:
             out.copy_(fn(X, delta=MOM_DELTA, check=False, **FILTER_ARGS))
         else:
@@ -119,10 +197,10 @@ AGG = {
     "bulyankrum": _bulyan_step("krum"),
     "bulyanmedian": _bulyan_step("median"),
     "bulyantrimmedmean": _bulyan_step("trimmedmean"),
-    "filterl2": _filter_step(engine.filter_l2),
-    "ex_noregret": _filter_step(engine.ex_noregret),
-    "mom_filterl2": _filter_step(engine.mom_filter_l2, mom=True),
-    "mom_ex_noregret": _filter_step(engine.mom_ex_noregret, mom=True),
+    "filterl2": _filter_step("filter_l2"),
+    "ex_noregret": _filter_step("ex_noregret"),
+    "mom_filterl2": _filter_step("mom_filter_l2", mom=True),
+    "mom_ex_noregret": _filter_step("mom_ex_noregret", mom=True),
 }
 OUT_DTYPE = {"bulyankrum": torch.float64, "bulyanmedian": torch.float64, "bulyantrimmedmean": torch.float64,
              "filterl2": torch.float64, "ex_noregret": torch.float64, "mom_filterl2": torch.float64,
@@ -344,6 +422,12 @@ def host_inclusive(agg, n, device):
 
 def main():
     a = parse()
+    rc = ranks_or_launch(a)
+    if rc is not None:
+        return rc
+    if a.launch_check:
+        return launch_check(a)
+    _load_engine()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -351,14 +435,12 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+        world = dist.get_world_size()
     n = a.clients
     d = int(a.d)
     # synthetic client updates, resident in HBM (fixed seed per rank)
-    g = torch.Generator(device=device).manual_seed(1234 + rank)
-    X = torch.empty((n, d), dtype=torch.float32, device=device)
-    rows_per = max(1, int(2e9 // (4 * d)) or 1)
-    for r0 in range(0, n, rows_per):
-        X[r0:r0 + rows_per].normal_(0.0, 0.01, generator=g)
+    byz = min(a.byzantine, max(n - 1, 0))
+    X = synthetic_rows(n, d, byz, 1234 + rank, device)
     odt = OUT_DTYPE.get(a.agg, torch.float32)
     out = torch.empty(d, dtype=odt, device=device)
     full = torch.empty(d * world, dtype=odt, device=device) if world > 1 else None
@@ -461,6 +543,7 @@ def main():
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
+        "world_size": world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
@@ -468,7 +551,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: N(0, 0.01) fp32 client updates generated on device",
+        "data": ("synthetic (SURVEY.md §8(d)), generated on device: 0.01 N(0,1) per client + shared 0.001 N(0,1) "
+                 "drift; rows 0..%d Byzantine at -10x the benign mean + 0.001 N(0,1)" % (byz - 1)
+                 if byz else "synthetic, generated on device: 0.01 N(0,1) + shared 0.001 N(0,1) drift, no "
+                 "Byzantine rows"),
         "config": {"workload": "%s N=%d clients x d=%.0e fp32 per GPU%s" % (
                        a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
@@ -502,4 +588,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -50,6 +50,12 @@ int sra_version(void);
  * (larger N goes through the LDS path). */
 int sra_max_register_clients(void);
 
+/* Number of device row indices (Krum / Bulyan selections, row gathers) found
+ * outside their matrix since the last reset; each was clamped to the matrix.
+ * Non-zero means a bug (the GPU tests assert 0).  Synchronous: waits for the
+ * device.  A library built with -DSRA_DEVICE_ASSERT traps instead. */
+int sra_row_fault_count(int32_t reset, uint32_t* count);
+
 /* ------------------------------------------------------------------------ */
 /* Coordinate-wise aggregators (k1: per-coordinate k-select)                 */
 /* ------------------------------------------------------------------------ */
@@ -109,9 +115,11 @@ int sra_krum_select_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32
 int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t rounds, int32_t* order, float* scores,
                        void* ws, size_t ws_bytes, void* stream);
 
-/* out[r, :] = X[rows[r], :] for r < nrows (rows is a device int32 array). */
-int sra_gather_rows_f32(const float* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows, float* out,
-                        int64_t ldo, void* stream);
+/* out[r, :] = X[rows[r], :] for r < nrows (rows is a device int32 array of
+ * indices into the n rows of X; an index outside [0, n) is clamped and counted,
+ * see sra_row_fault_count). */
+int sra_gather_rows_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows,
+                        float* out, int64_t ldo, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Median-of-means bucketing (k5)                                            */
@@ -138,11 +146,14 @@ int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32_t mode, si
  * whose nearest client is removed), then the per-coordinate Bulyan median
  * with numpy's fp64 pairwise tie-break and the mean of the beta = theta - 2f
  * nearest values.  out: d float64 values.  selected (optional, theta int32):
- * the chosen clients in krum mode.  theta <= 0 -> SRA_ERR_THETA.
- * 1 <= n <= 512 (more than 128 remaining clients: LDS k-select + distance
+ * the chosen clients in krum mode.  status (optional, one int32, written
+ * stream-ordered): 1 if a median / trimmed-mean round found no strict
+ * minimum distance -- every distance NaN / inf, where the reference's
+ * `assert min_index != None` (:308, :321) raises -- else 0.  theta <= 0 ->
+ * SRA_ERR_THETA.  1 <= n <= 512 (more than 128 remaining clients: LDS k-select + distance
  * passes per round; theta > 128: an LDS-sorted per-coordinate stage). */
 int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
-                   int32_t* selected, void* ws, size_t ws_bytes, void* stream);
+                   int32_t* selected, int32_t* status, void* ws, size_t ws_bytes, void* stream);
 
 
 /* One selection round of Bulyan's median / trimmed-mean modes
@@ -377,7 +388,7 @@ int sra_clip_scale_running_f32(const float* M, int64_t k, int64_t d, int64_t ldm
  * (= Krum with f + 1 over the others; f = 1 is rejected), median rounds take
  * the lower median.  The per-coordinate stage is shared (fp64). */
 int sra_bulyan_dba_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
-                       int32_t* selected, void* ws, size_t ws_bytes, void* stream);
+                       int32_t* selected, int32_t* status, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

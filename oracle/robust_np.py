@@ -322,7 +322,10 @@ def bulyan_select(rows, f, aggsubfunc):
                 dd = _l2(agg - r)
                 if dd < best_d:
                     best, best_d = pos, dd
-            assert best is not None
+            if best is None:
+                # every distance NaN / inf: `assert min_index != None`
+                # (robust_estimator.py:308, 321)
+                raise AssertionError("bulyan %s round: no finite distance" % aggsubfunc)
             removed.append(remaining.pop(best))
     return selected, removed
 
@@ -511,6 +514,19 @@ def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7,
     step = 0.5 / (np.amax(far[np.triu_indices(m, 1)]) ** 2)
     c = np.ones(m)
     for it in range(int(2 * eps * m)):
+        if c is None:
+            # the previous projection was infeasible (projected_c = None, :99):
+            # np.average(weights=None) is the plain fp32 mean, the covariance
+            # the fp32 mean of fp32 outer products, eigh in fp32 (:65-69); the
+            # early exit returns that mean (:71-72), otherwise the update
+            # c * (1 - step * tau) raises TypeError (:75)
+            mu32 = np.average(x, axis=0)
+            z32 = x - mu32
+            cov32 = np.average(np.array([np.outer(r, r) for r in z32]), axis=0)
+            lam32 = eigh(cov32, subset_by_index=[k - 1, k - 1], eigvals_only=True)[0]
+            if lam32 * lam32 <= expansion * sigma * sigma:
+                return mu32
+            raise TypeError("unsupported operand type(s) for *: 'NoneType' and 'float' (ex_noregret, :75)")
         c = _perturbed(c, perturb, it)
         mu = np.average(x, axis=0, weights=c)
         z = x - mu
@@ -525,8 +541,9 @@ def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7,
             rec["capped"].append(info["capped"])
             rec["margin"].append(info["margin"])
             rec["iters"] = it + 1
-        if c is None:
-            raise TypeError("ex_noregret: no feasible capped-simplex projection")
+    if c is None:
+        # infeasible at the last iteration: the final np.average(weights=None) (:101)
+        return np.average(x, axis=0)
     return np.average(x, axis=0, weights=c)
 
 

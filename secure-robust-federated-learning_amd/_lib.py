@@ -61,6 +61,7 @@ _SIGS = {
     "sra_last_error": [],
     "sra_version": [],
     "sra_max_register_clients": [],
+    "sra_row_fault_count": [_i32, ctypes.POINTER(ctypes.c_uint32)],
     "sra_average_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr],
     "sra_median_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr],
     "sra_trimmed_mean_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr],
@@ -69,10 +70,10 @@ _SIGS = {
     "sra_krum_workspace_bytes": [_i64, _i64, ctypes.POINTER(_sz)],
     "sra_krum_select_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
     "sra_krum_from_gram": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
-    "sra_gather_rows_f32": [_ptr, _i64, _i64, _ptr, _i32, _ptr, _i64, _ptr],
+    "sra_gather_rows_f32": [_ptr, _i64, _i64, _i64, _ptr, _i32, _ptr, _i64, _ptr],
     "sra_bucket_mean_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _i64, _ptr],
     "sra_bulyan_workspace_bytes": [_i64, _i64, _i32, _i32, ctypes.POINTER(_sz)],
-    "sra_bulyan_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_bulyan_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _ptr, _sz, _ptr],
     "sra_bulyan_coordinate_f64": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
     "sra_bulyan_stage_workspace_bytes": [_i64, _i64, ctypes.POINTER(_sz)],
     "sra_bulyan_round_workspace_bytes": [_i64, ctypes.POINTER(_sz)],
@@ -112,7 +113,7 @@ _SIGS = {
     "sra_weighted_sum_f32": [_ptr, _i64, _i64, _i64, _ptr, _ptr, _ptr],
     "sra_clip_scale_running_f32": [_ptr, _i64, _i64, _i64, _ptr, ctypes.POINTER(_i64), _i32, _dbl, _ptr, _ptr, _ptr,
                                    _sz, _ptr],
-    "sra_bulyan_dba_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_bulyan_dba_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _ptr, _sz, _ptr],
 }
 _RESTYPES = {"sra_last_error": ctypes.c_char_p}
 

@@ -49,17 +49,11 @@ __device__ __forceinline__ const char* uniform_ptr(const char* p) {
   return reinterpret_cast<const char*>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 
-// A row index taken from a device row list (by readlane from the list held in
-// VGPRs, or loaded): clamped to the matrix in SALU, so a stale or corrupt
-// entry cannot address outside it (round 2's one GPU fault was a readlane of a
-// register slot the compiler had written under a partial exec mask).  Builds
-// with -DSRA_DEVICE_ASSERT trap on it instead.
-__device__ __forceinline__ int checked_row(int row, int nrows) {
-#ifdef SRA_DEVICE_ASSERT
-  if (static_cast<unsigned>(row) >= static_cast<unsigned>(nrows)) __builtin_trap();
-#endif
-  return static_cast<int>(min(static_cast<unsigned>(row), static_cast<unsigned>(nrows - 1)));
-}
+// Row indices taken from device row lists (by readlane from the list held in
+// VGPRs, or loaded) go through checked_row (sra_common.hpp): round 2's one GPU
+// fault was a readlane of a register slot the compiler had written under a
+// partial exec mask.
+unsigned int bulyan_row_faults(bool reset) { return tu_row_faults(reset); }
 
 __device__ __forceinline__ float ld_lane(const char* row, unsigned off) {
   typedef const __attribute__((address_space(1))) float gfloat;
@@ -867,172 +861,6 @@ __global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(cons
 }
 
 // ---------------------------------------------------------------------------
-// Median-mode rounds with ONE read of the remaining rows per round (N <= 128,
-// not the DBA lower median).  Removing client k from a sorted column changes
-// its median to one of three neighbouring order statistics, so the pass of
-// round r -- which sorts the column of R_r anyway -- keeps them:
-//   median_pass_kernel<P, true>: per coordinate, load the column of R_r once;
-//     squared distances to agg_r (round r's aggregate, read back: 4 B per
-//     coordinate) with select_dist_rows_kernel's fp32 arithmetic; then the
-//     median network pruned to the padded slots P/2 - 2 .. P/2 and
-//     cand = (those three values, NaN count).
-//   bulyan_pick_kernel: k_r (also written out as the picked row).
-//   median_finish_kernel: agg_{r+1} = the median of R_r \ {x_k} from cand and
-//     x_k alone: n = |R_r| odd -> (c1 + c2), (c0 + c2) or (c0 + c1) times 0.5
-//     as x_k <= c0, <= c1 or above (NaN compares false: removed from the top,
-//     where the network put it as +inf); n even -> c2 if x_k <= c1 else c1;
-//     NaN if a NaN remains.  The same values and the same formula as sorting
-//     R_{r+1} (select_dist_rows_kernel): every aggregate, distance and pick is
-//     bit-identical to the fused two-read round.
-// Round 0 runs median_pass_kernel<P, false> (agg_0 + cand) and dist_rows_kernel.
-// ---------------------------------------------------------------------------
-template <int P, bool DIST>
-__global__ void __launch_bounds__(256, 3) median_pass_kernel(const float* __restrict__ X, int64_t ldx,
-                                                          const int* __restrict__ rows, int nrows_x, int n_arg,
-                                                          int64_t d, const float* __restrict__ agg_in,
-                                                          float* __restrict__ agg_out, f32x4* __restrict__ cand,
-                                                          float* __restrict__ bpart, int nb, int tpb) {
-  constexpr int P2 = next_pow2(P);
-  const unsigned t = threadIdx.x;
-  const unsigned lane = t & 63u;
-  const unsigned w = t >> 6;
-  constexpr int RW = (P + 63) / 64;
-  int rl[RW];
-#pragma unroll
-  for (int q = 0; q < RW; ++q) {
-    const int li = 64 * q + static_cast<int>(lane);
-    rl[q] = rows[li < n_arg ? li : n_arg - 1];
-  }
-  __shared__ float dl[4][32][68];
-  __shared__ float wsum[4][P];
-  float bs = 0.f;
-  const int n_out = n_arg;
-  const int64_t ntiles = cdiv(d, 256);
-  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * tpb;
-  const int64_t t1 = t0 + tpb < ntiles ? t0 + tpb : ntiles;
-  const unsigned ti = lane & 31u, th = lane >> 5;
-  for (int64_t tile = t0; tile < t1; ++tile) {
-    const int64_t base = tile * 256;
-    const int64_t rem = d - base;
-    const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
-    const unsigned tc = t < last ? t : last;
-    const unsigned off = tc * 4u;
-#pragma unroll
-    for (int q = 0; q < RW; ++q) asm volatile("" : "+v"(rl[q]));
-    int n = n_arg;
-    asm volatile("" : "+s"(n));
-    const int k_bottom = (P - n) / 2;
-    auto load = [&](int i) -> float {
-      const int row = checked_row(__builtin_amdgcn_readlane(rl[i / 64], i % 64), nrows_x);
-      const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
-      typedef const __attribute__((address_space(1))) float gfloat;
-      return __builtin_nontemporal_load(reinterpret_cast<gfloat*>(reinterpret_cast<uint64_t>(rp) + off));
-    };
-    constexpr int kFirstPad = P > 16 ? P - 16 : 0;
-    float v[P2];
-#pragma unroll
-    for (int i = 0; i < kFirstPad; ++i) {
-      v[i] = load(i);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int i = kFirstPad; i < P; ++i) {
-      const float x = load(i);
-      __builtin_amdgcn_sched_barrier(0);
-      const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
-      v[i] = i < n ? x : pad;
-    }
-    if constexpr (DIST) {
-      // squared distances to agg_r from the loaded column (rows >= n hold pads:
-      // their sums are never read), select_dist_rows_kernel's arithmetic
-      const float res = agg_in[base + tc];
-      const bool valid = t < rem;
-#pragma unroll
-      for (int c = 0; c < RW * 2; ++c) {
-        if (32 * c >= n) break;   // wave-uniform
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          if (32 * c + i < P) dl[w][i][lane] = valid ? res - v[32 * c + i] : 0.f;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        float sh = 0.f;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const f32x4 q = *reinterpret_cast<const f32x4*>(&dl[w][ti][32 * th + 4 * u]);
-          sh = __builtin_fmaf(q[0], q[0], sh);
-          sh = __builtin_fmaf(q[1], q[1], sh);
-          sh = __builtin_fmaf(q[2], q[2], sh);
-          sh = __builtin_fmaf(q[3], q[3], sh);
-        }
-        const float so = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(static_cast<int>((lane ^ 32u) * 4u),
-                                                                                __builtin_bit_cast(int, sh)));
-        const float st = th == 0 ? sh + so : so + sh;
-        if (th == 0 && 32 * c + static_cast<int>(ti) < n) wsum[w][32 * c + ti] = st;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
-    // NaN detection over all slots (pads are +-inf, never NaN)
-    float m = v[0];
-#pragma unroll
-    for (int i = 1; i < P; ++i) m = __builtin_elementwise_maximum(m, v[i]);
-    int nan_cnt = 0;
-    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {
-#pragma unroll
-      for (int i = 0; i < P; ++i) {
-        const bool isn = __builtin_isnan(v[i]);
-        nan_cnt += isn ? 1 : 0;
-        v[i] = isn ? __builtin_inff() : v[i];
-      }
-    }
-    network_fast<P2, P, P / 2 - 2, P / 2 + 1>(v);
-    if (t < rem) {
-      const f32x4 c4 = {v[P / 2 - 2], v[P / 2 - 1], v[P / 2], static_cast<float>(nan_cnt)};
-      cand[base + t] = c4;
-      if constexpr (!DIST) {
-        float res = (n & 1) ? v[P / 2 - 1] : (v[P / 2 - 1] + v[P / 2]) * 0.5f;
-        if (nan_cnt > 0) res = qnan();
-        agg_out[base + t] = res;
-      }
-    }
-    if constexpr (DIST) {
-      __syncthreads();
-      if (static_cast<int>(t) < n) bs += (wsum[0][t] + wsum[1][t]) + (wsum[2][t] + wsum[3][t]);
-      __syncthreads();
-    }
-  }
-  if constexpr (DIST) {
-    if (static_cast<int>(t) < n_out) bpart[static_cast<int64_t>(t) * nb + blockIdx.x] = bs;
-  }
-}
-
-// agg_{r+1} from round r's candidates and the removed row (see above); n = |R_r|
-__global__ void __launch_bounds__(256) median_finish_kernel(const float* __restrict__ X, int64_t ldx, int nrows_x,
-                                                            const int* __restrict__ picked,
-                                                            const f32x4* __restrict__ cand, int n, int64_t d,
-                                                            float* __restrict__ agg) {
-  const int k = checked_row(__builtin_amdgcn_readfirstlane(*picked), nrows_x);
-  const float* xk = X + static_cast<int64_t>(k) * ldx;
-  for (int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < d;
-       j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const f32x4 c = cand[j];
-    const float v = xk[j];
-    float res;
-    if (n & 1) {
-      res = v <= c[0] ? (c[1] + c[2]) * 0.5f : (v <= c[1] ? (c[0] + c[2]) * 0.5f : (c[0] + c[1]) * 0.5f);
-    } else {
-      res = v <= c[1] ? c[2] : c[1];
-    }
-    const int nanc = static_cast<int>(c[3]) - (__builtin_isnan(v) ? 1 : 0);
-    if (nanc > 0) res = qnan();
-    agg[j] = res;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // The stage for theta in (128, kBigMaxClients]: a 64-coordinate tile of pn =
 // next_pow2(theta) slots in LDS per 256-thread block, filled in selection
 // order through the row list, bitonic-sorted by the block; then one lane per
@@ -1205,7 +1033,6 @@ static size_t bulyan_body_bytes(int n, int64_t d, int mode, int f) {
   } else {
     b += sizeof(float) * static_cast<size_t>(theta > 0 ? theta : 0) * static_cast<size_t>(d) + 256;
     b += round_partial_bytes(n, d) + sizeof(double) * static_cast<size_t>(n) + 512;
-    if (mode == kBulyanMedian) b += 4 * sizeof(float) * static_cast<size_t>(d) + 256;   // median candidates
   }
   return (b + 255) / 256 * 256;
 }
@@ -1220,12 +1047,9 @@ static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int 
   const int64_t tpb = round_tiles_per_block(d);
   const int64_t blocks = round_blocks(d);
   const int P = static_cast<int>(cdiv(n, 16) * 16);
-  // SRA_ROUND_LDS: extra dynamic LDS per block, to cap the blocks per CU in
-  // A/B runs (tiles in flight per XCD vs the re-read's L2 hit rate)
-  static const int lds_pad = [] { const char* e = getenv("SRA_ROUND_LDS"); return e && *e ? atoi(e) : 0; }();
 #define SRA_SR(PP)                                                                                             \
   case PP:                                                                                                     \
-    hipLaunchKernelGGL((select_dist_rows_kernel<PP, MODE>), dim3(blocks), dim3(256), lds_pad, s, X, ldx, rows, nrows_x, n, \
+    hipLaunchKernelGGL((select_dist_rows_kernel<PP, MODE>), dim3(blocks), dim3(256), 0, s, X, ldx, rows, nrows_x, n,       \
                        d, lo,                                                                                  \
                        hi, out, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                       \
     return launch_status("select_dist_rows_kernel");
@@ -1352,7 +1176,7 @@ __global__ void iota_kernel(int* p, int n) {
 // other clients (identical while remaining - f - 2 >= 1: f >= 2 or f == 0); its median rounds take
 // torch.median's LOWER median (:1025); trimmed-mean rounds and theta / beta are unchanged.
 int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode, double* out, int* sel_out,
-                  void* ws, size_t ws_bytes, hipStream_t s, bool dba = false) {
+                  int* status_out, void* ws, size_t ws_bytes, hipStream_t s, bool dba = false) {
   const int theta = n - 2 * f;
   SRA_REQUIRE(theta > 0, SRA_ERR_THETA, "bulyan needs theta = N - 2f > 0 (N=%d, f=%d)", n, f);
   SRA_REQUIRE(mode >= 0 && mode <= 2, SRA_ERR_ARG, "bad bulyan mode %d", mode);
@@ -1363,7 +1187,10 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
   int* order = reinterpret_cast<int*>(p + 256);
   int* rows_a = order + n;
   int* rows_b = rows_a + n;
-  int* status = rows_b + n;
+  // status: 1 = a median / trimmed-mean round found no strict minimum (every
+  // distance NaN or inf): the reference's `assert min_index != None` (:308, :321)
+  int* status = status_out != nullptr ? status_out : rows_b + n;
+  SRA_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
   char* rest = p + 4096 + 4 * static_cast<size_t>(n) * 4;
   int* nf_count = reinterpret_cast<int*>(p);
   int64_t* nf_list = reinterpret_cast<int64_t*>(p + bulyan_body_bytes(n, d, mode, f));
@@ -1388,51 +1215,6 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
       (reinterpret_cast<uintptr_t>(bpart) + round_partial_bytes(n, d) + 255) & ~static_cast<uintptr_t>(255));
   int* cur = rows_a;
   int* nxt = rows_b;
-  // SRA_BULYAN_MEDIAN_1READ=1 takes the one-read median rounds (A/B against the fused two-read rounds)
-  static const int one_read = [] { const char* e = getenv("SRA_BULYAN_MEDIAN_1READ"); return e && *e ? atoi(e) : 0; }();
-  if (mode == kBulyanMedian && !dba && n <= 128 && one_read) {
-    f32x4* cand = reinterpret_cast<f32x4*>(
-        (reinterpret_cast<uintptr_t>(dist + n) + 255) & ~static_cast<uintptr_t>(255));
-    int* picked = status + 1;
-    const int64_t tpb = round_tiles_per_block(d);
-    const int64_t blocks = round_blocks(d);
-    for (int t = 0; t < theta; ++t) {
-      const int nr = n - t;
-      float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
-      const int P = static_cast<int>(cdiv(nr, 16) * 16);
-      if (t > 0) {
-        hipLaunchKernelGGL(median_finish_kernel, dim3(static_cast<unsigned>(cdiv(d, 256) < 4096 ? cdiv(d, 256) : 4096)),
-                           dim3(256), 0, s, X, ldx, n, picked, cand, nr + 1, d, agg);
-        rc = launch_status("median_finish_kernel");
-        if (rc) return rc;
-      }
-#define SRA_MP(PP)                                                                                                   case PP:                                                                                                             if (t == 0)                                                                                                          hipLaunchKernelGGL((median_pass_kernel<PP, false>), dim3(blocks), dim3(256), 0, s, X, ldx, cur, n, nr, d,                              nullptr, agg, cand, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                  else                                                                                                                 hipLaunchKernelGGL((median_pass_kernel<PP, true>), dim3(blocks), dim3(256), 0, s, X, ldx, cur, n, nr, d, agg,                          nullptr, cand, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                       break;
-      switch (P) {
-        SRA_MP(16) SRA_MP(32) SRA_MP(48) SRA_MP(64) SRA_MP(80) SRA_MP(96) SRA_MP(112) SRA_MP(128)
-        default: break;
-      }
-#undef SRA_MP
-      rc = launch_status("median_pass_kernel");
-      if (rc) return rc;
-      if (t == 0) {
-        hipLaunchKernelGGL(dist_rows_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, cur, n, nr, d, agg, bpart,
-                           static_cast<int>(blocks), static_cast<int>(tpb));
-        rc = launch_status("dist_rows_kernel");
-        if (rc) return rc;
-      }
-      hipLaunchKernelGGL(bulyan_dist_reduce_kernel, dim3(nr), dim3(256), 0, s, bpart,
-                         static_cast<int>(blocks), dist);
-      rc = launch_status("bulyan_dist_reduce_kernel");
-      if (rc) return rc;
-      hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, dist, cur, nr, nxt, status, picked);
-      rc = launch_status("bulyan_pick_kernel");
-      if (rc) return rc;
-      int* tmp = cur;
-      cur = nxt;
-      nxt = tmp;
-    }
-    return launch_final(S, d, order, theta, theta, beta, d, out, nf_count, nf_list, s);
-  }
   for (int t = 0; t < theta; ++t) {
     const int nr = n - t;
     float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
@@ -1460,22 +1242,24 @@ extern "C" int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32
 }
 
 extern "C" int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode,
-                              double* out, int32_t* selected, void* ws, size_t ws_bytes, void* stream) {
+                              double* out, int32_t* selected, int32_t* status, void* ws, size_t ws_bytes,
+                              void* stream) {
   SRA_REQUIRE(X != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
   SRA_REQUIRE(n >= 1 && n <= kBigMaxClients && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= %d)",
               kBigMaxClients);
-  return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
+  return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, status, ws, ws_bytes,
                        static_cast<hipStream_t>(stream));
 }
 
 extern "C" int sra_bulyan_dba_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode,
-                                  double* out, int32_t* selected, void* ws, size_t ws_bytes, void* stream) {
+                                  double* out, int32_t* selected, int32_t* status, void* ws, size_t ws_bytes,
+                                  void* stream) {
   SRA_REQUIRE(X != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
   SRA_REQUIRE(n >= 1 && n <= kBigMaxClients && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape (N <= %d)",
               kBigMaxClients);
   SRA_REQUIRE(!(mode == kBulyanKrum && f == 1), SRA_ERR_ARG,
               "DBA bulyan_krum with f = 1 (its last round scores an empty neighbour set) is not supported");
-  return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, ws, ws_bytes,
+  return launch_bulyan(X, static_cast<int>(n), d, ldx, f, mode, out, selected, status, ws, ws_bytes,
                        static_cast<hipStream_t>(stream), true);
 }
 

@@ -551,51 +551,34 @@ static int64_t num_cus() {
   return cus;
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return (e != nullptr && e[0] != 0) ? atoi(e) : dflt;
-}
-
-// Variant selection.  Defaults are the measured-fastest; the
-// SRA_SELECT (1 = generic one-lane network) and SRA_BS (block size) environment
-// variables exist for A/B measurements only.
+// Variant selection (the measured-fastest per shape).
 template <int MODE>
 static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, int hi, float* out,
                          hipStream_t s) {
-  static const int force = env_int("SRA_SELECT", 0);
-  static const int bs_env = env_int("SRA_BS", 0);
   const int P = static_cast<int>(cdiv(n, 16) * 16);
   const bool trim128 = MODE == kTrimmed && n == 128 && lo == 12 && hi == 116;
   const bool trim100 = MODE == kTrimmed && n == 100 && lo == 10 && hi == 90;
 
   // Exact-N trimmed mean: the VOP2 min/max network with a NaN pre-pass
   // (measured 1.5-2 % faster than the VOP3 NaN-propagating one at N = 128,
-  // d = 1e8; SRA_NET=0 selects the latter).  The median keeps the
-  // NaN-propagating network (no pre-pass, fewer VALU ops).
-  static const int net_plain = env_int("SRA_NET", 1);
-  if (net_plain == 1 && force == 0) {
+  // d = 1e8).  The median keeps the NaN-propagating network (no pre-pass,
+  // fewer VALU ops).
+  if constexpr (MODE == kTrimmed) {
     const int64_t blocks = cdiv(d, 256);
-    if constexpr (MODE == kTrimmed) {
-      if (trim128) {
-        hipLaunchKernelGGL((select_plain_kernel<MODE, 128, 12>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
-        return launch_status("select_plain_kernel");
-      }
-      if (trim100) {
-        hipLaunchKernelGGL((select_plain_kernel<MODE, 100, 10>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
-        return launch_status("select_plain_kernel");
-      }
+    if (trim128) {
+      hipLaunchKernelGGL((select_plain_kernel<MODE, 128, 12>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
+      return launch_status("select_plain_kernel");
+    }
+    if (trim100) {
+      hipLaunchKernelGGL((select_plain_kernel<MODE, 100, 10>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
+      return launch_status("select_plain_kernel");
     }
   }
   if (n <= 128) {
-    const int bs = bs_env == 768 ? 768 : 256;
 #define SRA_SEL1(PP, NXX, BXX)                                                                                   \
   do {                                                                                                           \
-    if (bs == 768)                                                                                               \
-      hipLaunchKernelGGL((select_reg_kernel<PP, MODE, NXX, BXX, 768>), dim3(cdiv(d, 768)), dim3(768), 0, s, X, n, \
-                         d, ldx, lo, hi, out);                                                                   \
-    else                                                                                                         \
-      hipLaunchKernelGGL((select_reg_kernel<PP, MODE, NXX, BXX, 256>), dim3(cdiv(d, 256)), dim3(256), 0, s, X, n, \
-                         d, ldx, lo, hi, out);                                                                   \
+    hipLaunchKernelGGL((select_reg_kernel<PP, MODE, NXX, BXX, 256>), dim3(cdiv(d, 256)), dim3(256), 0, s, X, n,   \
+                       d, ldx, lo, hi, out);                                                                     \
     return launch_status("select_reg_kernel");                                                                   \
   } while (0)
     if (trim128) SRA_SEL1(128, 128, 12);
@@ -626,13 +609,8 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
       // plain loads: with streaming loads the half line a wave leaves for its
       // neighbour was refetched (median 1.12x the algorithmic bytes, 7.03 ms;
       // plain 1.00x, 6.83 ms at d = 1.25e7)
-      static const int nt = env_int("SRA_QUAD_NT", 0);
-      if (nt == 0)
-        hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51, false>), dim3(cdiv(d, 64)),
-                           dim3(256), 0, s, X, n, d, ldx, lo, hi, out);
-      else
-        hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51>), dim3(cdiv(d, 64)), dim3(256),
-                           0, s, X, n, d, ldx, lo, hi, out);
+      hipLaunchKernelGGL((select_quad_kernel<4, MODE, 512, MODE == kMedian ? -1 : 51, false>), dim3(cdiv(d, 64)),
+                         dim3(256), 0, s, X, n, d, ldx, lo, hi, out);
     } else {
       hipLaunchKernelGGL((select_quad_kernel<4, MODE>), dim3(cdiv(d, 64)), dim3(256), 0, s, X, n, d, ldx, lo, hi,
                          out);

@@ -2214,7 +2214,9 @@ __global__ void __launch_bounds__(256) chunk_gram_big_kernel(const float* __rest
   }
 }
 
-// numpy pairwise fp32 sum of f(0..m), m <= 512 (two levels of splits)
+// numpy pairwise fp32 sum of f(0..m), m <= 512: numpy splits while a piece
+// holds more than 128 elements; from m <= 512 the largest piece after three
+// splits is <= 76, so three levels are exact (m = 505: 248 + (128 + (64 + 65)))
 template <typename F>
 __device__ float np_pw32_big(int m, F&& f) {
   auto blk = [&](int lo, int mm) -> float {
@@ -2234,11 +2236,17 @@ __device__ float np_pw32_big(int m, F&& f) {
     for (; i < mm; ++i) res += f(lo + i);
     return res;
   };
-  auto half = [&](int lo, int mm) -> float {
+  auto quarter = [&](int lo, int mm) -> float {
     if (mm <= 128) return blk(lo, mm);
     int q = mm / 2;
     q -= q % 8;
     return blk(lo, q) + blk(lo + q, mm - q);
+  };
+  auto half = [&](int lo, int mm) -> float {
+    if (mm <= 128) return blk(lo, mm);
+    int q = mm / 2;
+    q -= q % 8;
+    return quarter(lo, q) + quarter(lo + q, mm - q);
   };
   if (m <= 128) return blk(0, m);
   int m2 = m / 2;
@@ -2745,18 +2753,13 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<1, false>));
   SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
-  const void* lsolve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
-                                       : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>))
-                                 : (dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<1, true>)
-                                       : reinterpret_cast<const void*>(&lanczos_solve_kernel<1, false>));
+  const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
+                           : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
   SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLds)));
-  // ex_noregret stays on the re-orthogonalising kernel.  SRA_NOREGRET_PLAIN=1
-  // runs it on the plain solver with the in-kernel re-orthogonalising attempt
-  // (A/B only: 217 ms vs 327 ms at C4, the decisions agree but the C4 fixture
-  // chunk 1 lands 2.9e-3 of max from the reference, bound 2e-5, and two DBA
-  // fixtures miss rtol 1e-5; SRA_NOREGRET_WARM=1 also warm-starts it)
-  static const int noregret_plain = [] { const char* e = getenv("SRA_NOREGRET_PLAIN"); return e && *e ? atoi(e) : 0; }();
-  static const int noregret_warm = [] { const char* e = getenv("SRA_NOREGRET_WARM"); return e && *e ? atoi(e) : 0; }();
+  // ex_noregret stays on the re-orthogonalising kernel: on the plain solver
+  // (217 vs 327 ms at C4) every traced decision agreed, but the C4 fixture
+  // chunk 1 landed 2.9e-3 of max from the reference (bound 2e-5) and two DBA
+  // fixtures missed rtol 1e-5 (DESIGN k6)
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
     GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws};
@@ -2771,26 +2774,21 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("noregret_pre_kernel");
       if (rc) return rc;
     }
-    // check schedule of the plain solver (SRA_FCHECK / SRA_FADV: A/B runs only)
-    static const int first_off = [] { const char* e = getenv("SRA_FCHECK"); return e && *e ? atoi(e) : -8; }();
-    static const int max_adv = [] { const char* e = getenv("SRA_FADV"); return e && *e ? atoi(e) : kMaxAdvance; }();
+    // check schedule of the plain solver: first check 8 steps before the
+    // previous iteration's step count (-4: 186.5 ms, 0: 353 ms at C4, DESIGN k6)
+    constexpr int first_off = -8;
     SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
                  trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr, first_off,
-                 max_adv > 0 ? max_adv : 1, noregret_warm};
+                 kMaxAdvance, 0};
     SRA_HIP(hipMemsetAsync(fbc, 0, 8 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
-    if (mode == 1 && noregret_plain == 0) {
+    if (mode == 1) {
       // round 2: ex_noregret's top two eigenvalues close in (gaps ~1e-3 after a
       // few iterations) and plain Lanczos without the re-orthogonalising
       // attempt stalled above the accuracy floor in a third of the chunks:
       // every chunk on the re-orthogonalising solver
       hipLaunchKernelGGL(list_all_kernel, dim3(cdiv(nb, 256)), dim3(256), 0, s, fbl, fbc, nb);
       rc = launch_status("list_all_kernel");
-      if (rc) return rc;
-    } else if (mode == 1) {
-      if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<1, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
-      else hipLaunchKernelGGL((lanczos_solve_kernel<1, false>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
-      rc = launch_status("lanczos_solve_kernel");
       if (rc) return rc;
     } else {
       if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<0, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);

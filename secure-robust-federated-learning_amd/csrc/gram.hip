@@ -451,16 +451,8 @@ int gram_num_wg(int64_t d) {
 // 4 waves (one per SIMD, all tiles of a k-step in one wave: the fragments are
 // centred and split once per wave) for N <= 128 -- measured 1.43 vs 1.50 ms
 // for 8 waves at N = 128, d = 1e7; 8 waves for larger N (the 4-wave tile
-// groups would need more accumulators than a wave holds).  SRA_GRAM_WAVES=4|8
-// overrides, for A/B runs.
-static int gram_waves(int nb) {
-  static const int force = [] {
-    const char* e = getenv("SRA_GRAM_WAVES");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  if (force == 4 || force == 8) return force;
-  return nb <= 4 ? 4 : 8;
-}
+// groups would need more accumulators than a wave holds).
+static constexpr int gram_waves(int nb) { return nb <= 4 ? 4 : 8; }
 
 // pair: (off_a, off_b, split, ldg, write_aa, write_bb) of the pair path, or
 // nullptr for a whole matrix of n <= 256 rows
@@ -486,7 +478,7 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
     static_assert(NB == 4 && WAVES == 4 && STG == 0, "pipelined Gram: N in (96, 128], four waves");
     SRA_REQUIRE(pr == nullptr && n == 128 && vec && d % C::STAGE == 0, SRA_ERR_ARG,
                 "pipelined Gram needs N == 128, aligned rows and d %% %d == 0", C::STAGE);
-    const int rc0 = launch_gram_pipe(X, n, d, ldx, slab, nwg, PF, s);
+    const int rc0 = launch_gram_pipe(X, n, d, ldx, slab, nwg, s);
     if (rc0) return rc0;
   } else if (vec) {
     SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_partial_kernel<NB, WAVES, true, STG, PF, WM>),
@@ -515,41 +507,27 @@ static int launch_gram_nbw(const float* X, int n, int64_t d, int64_t ldx, double
   return launch_status("gram_reduce2_kernel");
 }
 
+// Kernel choice (DESIGN k2; the losing variants of rounds 2-3 -- two register
+// stage sets, 64-coordinate stages, eight-wave per-wave means, phase-B loads --
+// are recorded there and no longer built):
+//   N == 128, 16-byte aligned rows, d % 128 == 0, 32-bit row offsets: the
+//     software-pipelined kernel (gram_pipe.hip);
+//   other N <= 128 without a pair: four waves with per-wave column means;
+//   pairs (N > 256) and N > 128: the partial-sum means kernel.
 template <int NB>
 static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double* G, float* slab, hipStream_t s,
                           const GramPair* pr = nullptr) {
-  // SRA_GRAM_STAGE64=1: 64-coordinate stages for N <= 128, half the LDS, two
-  // workgroups per CU (A/B runs)
-  static const int st64 = [] { const char* e = getenv("SRA_GRAM_STAGE64"); return e && *e ? atoi(e) : 0; }();
-  // SRA_GRAM_V (N <= 128, unpaired; A/B runs, DESIGN k2): default -1 = the
-  // pipelined kernel with phase-A loads where it applies (N == 128, aligned
-  // rows, d % 128 == 0), per-wave means elsewhere; 0 round 2's kernel (one
-  // register stage set, partial-sum means, two barriers per stage); 1 two
-  // stage sets in flight; 2 two sets + per-wave means; 3 per-wave means;
-  // 4 per-wave means on eight waves; 5 / 6 pipelined with phase-B / phase-A
-  // loads; 7 pipelined without stage loads (timing only: WRONG results)
-  static const int gv = [] { const char* e = getenv("SRA_GRAM_V"); return e && *e ? atoi(e) : -1; }();
   if constexpr (NB <= 4) {
-    if (st64 == 1 && gram_waves(NB) == 4) return launch_gram_nbw<NB, 4, 64>(X, n, d, ldx, G, slab, s, pr);
-    if (pr == nullptr && gram_waves(NB) == 4) {
+    if (pr == nullptr) {
       if constexpr (NB == 4) {
         const bool aligned = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-        if ((gv == -1 || (gv >= 5 && gv <= 7)) && n == 128 && aligned && d % 128 == 0) {
-          if (gv == 5) return launch_gram_nbw<4, 4, 0, 0, true, true>(X, n, d, ldx, G, slab, s, pr);
-          if (gv == 7) return launch_gram_nbw<4, 4, 0, 2, true, true>(X, n, d, ldx, G, slab, s, pr);
+        if (n == 128 && aligned && d % 128 == 0 && gram_pipe_offsets_fit(ldx))
           return launch_gram_nbw<4, 4, 0, 1, true, true>(X, n, d, ldx, G, slab, s, pr);
-        }
       }
-      if (gv == 0) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
-      if (gv == 1) return launch_gram_nbw<NB, 4, 0, 2, false>(X, n, d, ldx, G, slab, s, pr);
-      if (gv == 2) return launch_gram_nbw<NB, 4, 0, 2, true>(X, n, d, ldx, G, slab, s, pr);
-      if (gv == 4) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
       return launch_gram_nbw<NB, 4, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
     }
   }
-  if (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
-  // SRA_GRAM_V=8 (A/B): per-wave means on the eight-wave kernels too (N > 128, unpaired)
-  if (gv == 8 && pr == nullptr) return launch_gram_nbw<NB, 8, 0, 1, true>(X, n, d, ldx, G, slab, s, pr);
+  if constexpr (gram_waves(NB) == 4) return launch_gram_nbw<NB, 4>(X, n, d, ldx, G, slab, s, pr);
   return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s, pr);
 }
 

@@ -84,8 +84,12 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// gram_pipe.hip: the software-pipelined N = 128 Gram (lm = where the next-but-one
-// stage's loads go: 0 phase B, 1 phase A, 2 none -- timing only)
-int launch_gram_pipe(const float* X, int n, int64_t d, int64_t ldx, float* slab, int nwg, int lm, hipStream_t s);
+// gram_pipe.hip: the software-pipelined N = 128 Gram.  Every row is addressed
+// by a 32-bit byte offset from one SGPR base (rows 0..7 of a load group, plus a
+// 128-coordinate stage), so the pipe kernel is taken only when those offsets fit.
+__host__ __device__ constexpr bool gram_pipe_offsets_fit(int64_t ldx) {
+  return ldx >= 0 && 7 * ldx * 4 + 4 * 128 < (int64_t(1) << 31);
+}
+int launch_gram_pipe(const float* X, int n, int64_t d, int64_t ldx, float* slab, int nwg, hipStream_t s);
 
 }  // namespace sra

@@ -33,7 +33,6 @@ struct GramOps {
 // d a multiple of the 128-coordinate stage, so every load is a full, guard-free
 // float4 and the loop body is one basic block (no branch for sched_barrier to
 // stop at); past the last stage the loads re-read the last stage (discarded).
-template <int LM>
 __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
                                                float* __restrict__ slab, float* lds) {
   using C = GramCfg<4, 4, 0>;
@@ -161,7 +160,7 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
         prep_piece(ic, b, kg + 4, opB);
       } else if constexpr (i < 59) {
         store_one(bn, i - 43);
-        if constexpr (LM == 1) load_one(k2, i - 43);
+        load_one(k2, i - 43);
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -171,7 +170,6 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
       constexpr int i = decltype(ic)::value;
       mfma_slot(ic, opB);
       if constexpr (i < 43) prep_piece(ic, bn, kg, opA);
-      else if constexpr (i < 59 && LM == 0) load_one(k2, i - 43);
       __builtin_amdgcn_sched_barrier(0);
     });
   }
@@ -188,29 +186,25 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
   }
 }
 
-// LM: where the next-but-one stage's loads are issued (0: phase B, 1: phase A
-// right behind the stores, 1.5 phases ahead of their use; 2: not at all --
-// timing experiment only, the result is wrong)
-template <int LM>
+// the next-but-one stage's loads are issued in phase A right behind the
+// stores, 1.5 phases ahead of their use (phase-B loads measured 1.53 vs 1.48 ms)
 __global__ void __launch_bounds__(256) gram_pipe_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
                                                         float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  gram_body_pipe<LM>(X, n, d, ldx, slab, lds);
+  gram_body_pipe(X, n, d, ldx, slab, lds);
 }
 
-int launch_gram_pipe(const float* X, int n, int64_t d, int64_t ldx, float* slab, int nwg, int lm, hipStream_t s) {
+int launch_gram_pipe(const float* X, int n, int64_t d, int64_t ldx, float* slab, int nwg, hipStream_t s) {
   using C = GramCfg<4, 4, 0>;
   SRA_REQUIRE(n == 128 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 && d % C::STAGE == 0,
               SRA_ERR_ARG, "pipelined Gram needs N == 128, aligned rows and d %% %d == 0", C::STAGE);
+  SRA_REQUIRE(gram_pipe_offsets_fit(ldx), SRA_ERR_ARG,
+              "pipelined Gram: the 32-bit lane offsets cannot address rows %lld floats apart", (long long)ldx);
   const size_t lds = sizeof(float) * 2 * C::BUF;
-  auto go = [&](const void* kern, auto fn) {
-    SRA_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL(fn, dim3(nwg), dim3(256), lds, s, X, n, d, ldx, slab);
-    return SRA_OK;
-  };
-  if (lm == 1) return go(reinterpret_cast<const void*>(&gram_pipe_kernel<1>), gram_pipe_kernel<1>);
-  if (lm == 2) return go(reinterpret_cast<const void*>(&gram_pipe_kernel<2>), gram_pipe_kernel<2>);
-  return go(reinterpret_cast<const void*>(&gram_pipe_kernel<0>), gram_pipe_kernel<0>);
+  SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_pipe_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  hipLaunchKernelGGL(gram_pipe_kernel, dim3(nwg), dim3(256), lds, s, X, n, d, ldx, slab);
+  return SRA_OK;
 }
 
 }  // namespace sra

@@ -24,57 +24,106 @@ constexpr int kMaxClients = 512;
 // numpy's pairwise summation (numpy/_core/src/umath/loops_utils.h.src) for
 // float32, n elements at a[0..n): < 8 sequential from 0; <= 128 eight
 // accumulators then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail;
-// otherwise split at n/2 rounded down to a multiple of 8.
-template <int DEPTH>
-__device__ float np_pairwise_f32(const float* a, int n) {
-  if (n < 8) {
-    float res = 0.f;
-    for (int i = 0; i < n; ++i) res += a[i];
-    return res;
-  }
-  if (n <= 128 || DEPTH == 0) {
-    float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8) {
-      r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
-      r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
-    }
-    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < n; ++i) res += a[i];
-    return res;
-  }
-  if constexpr (DEPTH > 0) {
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    return np_pairwise_f32<DEPTH - 1>(a, n2) + np_pairwise_f32<DEPTH - 1>(a + n2, n - n2);
-  }
-  return 0.f;
-}
+// otherwise split at n/2 rounded down to a multiple of 8 (wave_pairwise_f32).
 
-// distance matrix (fp32) from the fp64 Gram
-__global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __restrict__ D) {
+// distance matrix (fp32) from the fp64 Gram.  A non-finite diagonal entry
+// means a NaN / inf somewhere in the data (the centring spreads it over every
+// entry): *nonfinite is set and the exact per-pair route below takes over.
+// acc (n x n fp64, optional) is zeroed for that route.
+__global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __restrict__ D, int* __restrict__ nonfinite,
+                                 double* __restrict__ acc) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * n) return;
   const int i = e / n, j = e - (e / n) * n;
   double sq = G[(int64_t)i * n + i] + G[(int64_t)j * n + j] - 2.0 * G[e];
-  if (i == j) sq = 0.0;
+  if (i == j) {
+    if (nonfinite != nullptr && !__builtin_isfinite(G[e])) atomicOr(nonfinite, 1);
+    sq = 0.0;
+  }
+  // a squared distance near fp32's range: the reference's fp32 norm overflows
+  if (nonfinite != nullptr && sq > 3.0e38) atomicOr(nonfinite, 1);
+  if (acc != nullptr) acc[e] = 0.0;
   D[e] = static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
 }
 
+// The exact route for data with NaN / inf (or fp32-overflowing distances):
+// acc[i][j] (i < j) = sum_k fp32(x_ik - x_jk)^2 in fp64 -- the reference's
+// np.linalg.norm of the fp32 difference (robust_estimator.py:242), whose NaN /
+// inf classes (a NaN anywhere, inf - inf = NaN, inf - finite = inf) IEEE
+// arithmetic reproduces; the pair's fp32 distance is sqrt(fp32(acc)).  Runs
+// only when krum_dist_kernel flagged the Gram (every block exits at once
+// otherwise).  Grid: (32 x 32 row-tile pairs I <= J) x d-slices; each thread
+// owns 4 pairs of its tile pair, fp64 partials added atomically.
+constexpr int kDirTile = 32;
+constexpr int kDirK = 64;
+__global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                                          const int* __restrict__ nonfinite,
+                                                          double* __restrict__ acc, int nslices) {
+  if (*nonfinite == 0) return;
+  __shared__ float ta[kDirTile][kDirK + 1];
+  __shared__ float tb[kDirTile][kDirK + 1];
+  const int nt = static_cast<int>(cdiv(n, kDirTile));
+  int I = 0, rem = blockIdx.y;
+  while (rem >= nt - I) { rem -= nt - I; ++I; }
+  const int J = I + rem;
+  const int tid = threadIdx.x;
+  const int ti = tid >> 3;              // row of tile I
+  const int tj = (tid & 7) * 4;         // first of 4 rows of tile J
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t per = cdiv(cdiv(d, kDirK), nslices) * kDirK;
+  const int64_t k0 = static_cast<int64_t>(blockIdx.x) * per;
+  const int64_t k1 = k0 + per < d ? k0 + per : d;
+  for (int64_t kb = k0; kb < k1; kb += kDirK) {
+    for (int e = tid; e < kDirTile * kDirK; e += 256) {
+      const int r = e / kDirK, c = e % kDirK;
+      const int64_t k = kb + c;
+      const int ra = I * kDirTile + r, rb = J * kDirTile + r;
+      ta[r][c] = (ra < n && k < k1) ? X[static_cast<int64_t>(ra) * ldx + k] : 0.f;
+      tb[r][c] = (rb < n && k < k1) ? X[static_cast<int64_t>(rb) * ldx + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int c = 0; c < kDirK; ++c) {
+      const float a = ta[ti][c];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double df = static_cast<double>(a - tb[tj + q][c]);   // the fp32 difference, squared in fp64
+        s[q] = fma(df, df, s[q]);
+      }
+    }
+    __syncthreads();
+  }
+  const int i = I * kDirTile + ti;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = J * kDirTile + tj + q;
+    if (i < n && j < n && (I < J || i < j)) atomicAdd(&acc[static_cast<int64_t>(i) * n + j], s[q]);
+  }
+}
+
 // Sort every row's off-diagonal distances ascending (ties by j): one workgroup
-// per row, bitonic network in LDS over next_pow2(n-1) slots.
+// per row, bitonic network in LDS over next_pow2(n-1) slots.  With the exact
+// route flagged, the distances come from acc instead of D.
 __global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restrict__ D, int n,
-                                                           float* __restrict__ S, int* __restrict__ J) {
+                                                           float* __restrict__ S, int* __restrict__ J,
+                                                           const int* __restrict__ nonfinite,
+                                                           const double* __restrict__ acc) {
   __shared__ float kv[kMaxClients];
   __shared__ int kj[kMaxClients];
   const int i = blockIdx.x;
   const int m = n - 1;
+  const bool direct = nonfinite != nullptr && *nonfinite != 0;
   int pn = 1;
   while (pn < m) pn <<= 1;
   for (int p = threadIdx.x; p < pn; p += blockDim.x) {
     if (p < m) {
       const int j = p < i ? p : p + 1;
-      kv[p] = D[(int64_t)i * n + j];
+      if (direct) {
+        const double sq = i < j ? acc[(int64_t)i * n + j] : acc[(int64_t)j * n + i];
+        kv[p] = sqrtf(static_cast<float>(sq));   // np.sqrt of the fp32 squared norm (inf on fp32 overflow)
+      } else {
+        kv[p] = D[(int64_t)i * n + j];
+      }
       kj[p] = j;
     } else {
       kv[p] = __builtin_inff();
@@ -137,14 +186,22 @@ __device__ __forceinline__ float wave_pw_block_f32(const float* a, int n) {
   return res;
 }
 
-// np_pairwise_f32 over one wave (n <= 512: at most two levels of splits)
+// np_pairwise_f32 over one wave, n <= 512.  numpy splits while a piece holds
+// more than 128 elements; from n <= 512 the largest piece after three splits
+// is <= 76, so three levels are exact (n = 505: 248 + (128 + (64 + 65))).
 __device__ __forceinline__ float wave_pairwise_f32(const float* a, int n) {
   if (n <= 128) return wave_pw_block_f32(a, n);
-  auto half = [&](const float* b, int m) -> float {
+  auto quarter = [&](const float* b, int m) -> float {
     if (m <= 128) return wave_pw_block_f32(b, m);
     int q = m / 2;
     q -= q % 8;
     return wave_pw_block_f32(b, q) + wave_pw_block_f32(b + q, m - q);
+  };
+  auto half = [&](const float* b, int m) -> float {
+    if (m <= 128) return wave_pw_block_f32(b, m);
+    int q = m / 2;
+    q -= q % 8;
+    return quarter(b, q) + quarter(b + q, m - q);
   };
   int n2 = n / 2;
   n2 -= n2 % 8;
@@ -291,13 +348,16 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
   }
 }
 
-// out[:] = X[order[sel], :] (the chosen client's row), and optional gathered rows
-__global__ void gather_rows_kernel(const float* __restrict__ X, int64_t d, int64_t ldx, const int* __restrict__ order,
-                                   int nrows, float* __restrict__ out, int64_t ldo) {
+unsigned int krum_row_faults(bool reset) { return tu_row_faults(reset); }
+
+// out[r, :] = X[order[r], :] (the chosen clients' rows); the index is checked
+// against the n rows of X
+__global__ void gather_rows_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                   const int* __restrict__ order, int nrows, float* __restrict__ out, int64_t ldo) {
   const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int r = blockIdx.y;
   if (j >= d || r >= nrows) return;
-  const int src = order[r];
+  const int src = checked_row(order[r], n);
   out[r * ldo + j] = X[static_cast<int64_t>(src) * ldx + j];
 }
 
@@ -305,23 +365,38 @@ size_t krum_workspace_bytes(int n, int64_t d);
 size_t gram_workspace_bytes(int n, int64_t d);
 int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes, hipStream_t s);
 
-// workspace layout: [G fp64 n*n][D n*n][S n*n][J n*n][gram slab]
+// workspace layout: [flag (256 B)][G fp64 n*n][acc fp64 n*n][D n*n][S n*n][J n*n][gram slab]
 size_t krum_workspace_bytes(int n, int64_t d) {
   const size_t nn = static_cast<size_t>(n) * n;
-  return 256 + nn * 8 + nn * 4 * 3 + gram_workspace_bytes(n, d);
+  return 256 + nn * 8 * 2 + nn * 4 * 3 + gram_workspace_bytes(n, d);
 }
 
-int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int* order, float* scores0,
-                                 char* ws, hipStream_t s) {
+// X (optional): the data G came from; with it, a non-finite G switches the
+// distances to the exact per-pair route (krum_direct_kernel), nonfinite / acc
+// its flag and n x n fp64 accumulator
+static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* order, float* scores0, char* ws,
+                              const float* X, int64_t d, int64_t ldx, int* nonfinite, double* acc, hipStream_t s) {
   const size_t nn = static_cast<size_t>(n) * n;
   float* D = reinterpret_cast<float*>(ws);
   float* S = D + nn;
   int* J = reinterpret_cast<int*>(S + nn);
-  hipLaunchKernelGGL(krum_dist_kernel, dim3(cdiv(n * n, 256)), dim3(256), 0, s, G, n, D);
+  if (X != nullptr) SRA_HIP(hipMemsetAsync(nonfinite, 0, sizeof(int), s));
+  hipLaunchKernelGGL(krum_dist_kernel, dim3(cdiv(n * n, 256)), dim3(256), 0, s, G, n, D, X ? nonfinite : nullptr,
+                     X ? acc : nullptr);
   int rc = launch_status("krum_dist_kernel");
   if (rc) return rc;
+  if (X != nullptr && n > 1) {
+    const int nt = static_cast<int>(cdiv(n, kDirTile));
+    const int64_t kb = cdiv(d, kDirK);
+    const int slices = static_cast<int>(kb < 256 ? kb : 256);
+    hipLaunchKernelGGL(krum_direct_kernel, dim3(slices, nt * (nt + 1) / 2), dim3(256), 0, s, X, n, d, ldx,
+                       nonfinite, acc, slices);
+    rc = launch_status("krum_direct_kernel");
+    if (rc) return rc;
+  }
   if (n > 1) {
-    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), 0, s, D, n, S, J);
+    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), 0, s, D, n, S, J, X ? nonfinite : nullptr,
+                       X ? acc : nullptr);
     rc = launch_status("krum_rowsort_kernel");
     if (rc) return rc;
   }
@@ -358,6 +433,11 @@ int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int*
   return launch_status("krum_rounds_kernel");
 }
 
+int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int* order, float* scores0,
+                                 char* ws, hipStream_t s) {
+  return launch_krum_rounds(G, n, f, rounds, order, scores0, ws, nullptr, 0, 0, nullptr, nullptr, s);
+}
+
 int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds, int* order, float* scores0,
                 void* ws, size_t ws_bytes, hipStream_t s) {
   SRA_REQUIRE(n >= 1 && n <= kMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d (got %d)", kMaxClients, n);
@@ -366,12 +446,14 @@ int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds
               "Krum workspace too small: need %zu bytes", krum_workspace_bytes(n, d));
   const size_t nn = static_cast<size_t>(n) * n;
   char* base = static_cast<char*>(ws);
+  int* nonfinite = reinterpret_cast<int*>(base);
   double* G = reinterpret_cast<double*>(base + 256);
-  char* rest = reinterpret_cast<char*>(G + nn);
+  double* acc = G + nn;
+  char* rest = reinterpret_cast<char*>(acc + nn);
   char* slab = rest + nn * 4 * 3;
   int rc = launch_gram(X, n, d, ldx, G, slab, gram_workspace_bytes(n, d), s);
   if (rc) return rc;
-  return launch_krum_rounds_from_gram(G, n, f, rounds, order, scores0, rest, s);
+  return launch_krum_rounds(G, n, f, rounds, order, scores0, rest, X, d, ldx, nonfinite, acc, s);
 }
 
 }  // namespace sra
@@ -403,11 +485,12 @@ extern "C" int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t
                                       static_cast<hipStream_t>(stream));
 }
 
-extern "C" int sra_gather_rows_f32(const float* X, int64_t d, int64_t ldx, const int32_t* rows, int32_t nrows,
-                                   float* out, int64_t ldo, void* stream) {
+extern "C" int sra_gather_rows_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const int32_t* rows,
+                                   int32_t nrows, float* out, int64_t ldo, void* stream) {
   SRA_REQUIRE(X != nullptr && rows != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
-  SRA_REQUIRE(nrows >= 1 && d >= 1 && ldo >= d && ldx >= d, SRA_ERR_SHAPE, "bad gather shape");
+  SRA_REQUIRE(n >= 1 && n <= (int64_t(1) << 30) && nrows >= 1 && d >= 1 && ldo >= d && ldx >= d, SRA_ERR_SHAPE,
+              "bad gather shape");
   hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(d, 256), nrows), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     X, d, ldx, rows, nrows, out, ldo);
+                     X, static_cast<int>(n), d, ldx, rows, nrows, out, ldo);
   return launch_status("gather_rows_kernel");
 }

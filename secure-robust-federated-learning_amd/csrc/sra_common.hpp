@@ -47,6 +47,40 @@ inline int launch_status(const char* what) {
 
 constexpr int kWave = 64;
 
+// ---------------------------------------------------------------------------
+// Row indices read from device row lists (Krum / Bulyan selections, gathers)
+// go through checked_row: an index outside the matrix is clamped so it cannot
+// address outside it, AND counted in this translation unit's fault counter
+// (a vector atomic), which sra_row_fault_count() reports -- the GPU tests
+// assert it stays 0.  Built with -DSRA_DEVICE_ASSERT (make DEVICE_ASSERT=1)
+// the kernel traps on it instead.
+// ---------------------------------------------------------------------------
+static __device__ unsigned int g_row_faults;
+
+__device__ __forceinline__ int checked_row(int row, int nrows) {
+  if (static_cast<unsigned>(row) >= static_cast<unsigned>(nrows)) {
+#ifdef SRA_DEVICE_ASSERT
+    __builtin_trap();
+#else
+    atomicAdd(&g_row_faults, 1u);
+#endif
+  }
+  return static_cast<int>(min(static_cast<unsigned>(row), static_cast<unsigned>(nrows - 1)));
+}
+
+// this translation unit's fault count (and reset); synchronous
+static inline unsigned int tu_row_faults(bool reset) {
+  unsigned int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_row_faults), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (reset) {
+    const unsigned int z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_row_faults), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  return v;
+}
+unsigned int krum_row_faults(bool reset);
+unsigned int bulyan_row_faults(bool reset);
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 

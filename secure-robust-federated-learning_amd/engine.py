@@ -134,9 +134,18 @@ def gather_rows(X, rows, out=None):
     k = int(rows.numel())
     if out is None:
         out = torch.empty((k, d), dtype=torch.float32, device=X.device)
-    _lib.call("sra_gather_rows_f32", X.data_ptr(), d, ldx, rows.data_ptr(), k, out.data_ptr(), out.stride(0),
+    _lib.call("sra_gather_rows_f32", X.data_ptr(), n, d, ldx, rows.data_ptr(), k, out.data_ptr(), out.stride(0),
               _stream_ptr(X.device))
     return out
+
+
+def row_fault_count(reset=True):
+    """Device row indices found outside their matrix (clamped) since the last
+    reset (sra_row_fault_count); synchronous.  Non-zero means a bug."""
+    import ctypes
+    c = ctypes.c_uint32(0)
+    _lib.call("sra_row_fault_count", int(bool(reset)), ctypes.byref(c))
+    return int(c.value)
 
 
 def krum(X, f):
@@ -170,9 +179,13 @@ def mom_krum(X, f, bucket_size=3):
 BULYAN_MODES = {"krum": 0, "median": 1, "trimmedmean": 2}
 
 
-def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
+def bulyan(X, f, aggsubfunc="trimmedmean", selected=False, check=True):
     """robust_estimator.bulyan on device: float64 (d,) aggregate.
-    With selected=True also returns the theta chosen clients (krum mode)."""
+    With selected=True also returns the theta chosen clients (krum mode).
+    check=True reads the selection status back (one host synchronisation) and
+    raises AssertionError where the reference's ``assert min_index != None``
+    fails (robust_estimator.py:308, 321): a median / trimmed-mean round whose
+    distances are all NaN / inf, e.g. bulyan(..., 'median') with a NaN client."""
     X, n, d, ldx = as_matrix(X)
     if aggsubfunc not in BULYAN_MODES:
         raise ValueError("aggsubfunc must be one of %s" % sorted(BULYAN_MODES))
@@ -180,10 +193,15 @@ def bulyan(X, f, aggsubfunc="trimmedmean", selected=False):
     theta = n - 2 * int(f)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
     sel = torch.empty(max(theta, 1), dtype=torch.int32, device=X.device) if selected else None
+    status = torch.empty(1, dtype=torch.int32, device=X.device)
     nb = _lib.query_bytes("sra_bulyan_workspace_bytes", n, d, int(f), mode)
     ws = _workspace(nb, X.device)
     _lib.call("sra_bulyan_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
-              sel.data_ptr() if sel is not None else None, ws.data_ptr(), nb, _stream_ptr(X.device))
+              sel.data_ptr() if sel is not None else None, status.data_ptr(), ws.data_ptr(), nb,
+              _stream_ptr(X.device))
+    if check and int(status.item()) == 1:
+        raise AssertionError("bulyan(%s): a selection round found no finite distance (min_index is None)"
+                             % aggsubfunc)
     return (out, sel) if selected else out
 
 
@@ -487,5 +505,5 @@ def bulyan_dba(X, f, aggsubfunc="trimmedmean", selected=False):
     nb = _lib.query_bytes("sra_bulyan_workspace_bytes", n, d, int(f), mode)
     ws = _workspace(nb, X.device)
     _lib.call("sra_bulyan_dba_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
-              sel.data_ptr() if sel is not None else None, ws.data_ptr(), nb, _stream_ptr(X.device))
+              sel.data_ptr() if sel is not None else None, None, ws.data_ptr(), nb, _stream_ptr(X.device))
     return (out, sel) if selected else out

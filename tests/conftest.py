@@ -93,3 +93,16 @@ def assert_chunks_within_bound(got, rec):
         sl = slice(c * itv, (c + 1) * itv)
         err = np.abs(got[sl] - want[sl]).max() / np.abs(want[sl]).max()
         assert err <= b, "%s chunk %d: %.3e of max > bound %.3e" % (rec["name"], c, err, b)
+
+
+@pytest.fixture(autouse=True)
+def _no_row_faults(request):
+    """Every GPU test ends with libsra's row-fault counter at 0: a device row
+    index outside its matrix is clamped in release builds and counted
+    (sra_row_fault_count), so a silent wrong-row read fails the test here."""
+    yield
+    if request.node.get_closest_marker("gpu") is None or not gpu_available():
+        return
+    import srfl_amd.engine as engine
+    n = engine.row_fault_count(reset=True)
+    assert n == 0, "%d device row indices were outside their matrix (clamped)" % n

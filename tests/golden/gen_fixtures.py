@@ -74,6 +74,103 @@ def run_case(ref, name, func, params, clients, call):
     _ = t
 
 
+def _none_exit_sigma(ref, xs, eps, expansion, itv):
+    """A sigma at which ex_noregret's projection is infeasible at iteration 0
+    (projected_c is None) and the next iteration -- weights=None, i.e. the
+    unweighted mean -- takes the early exit (robust_estimator.py:65-72, 99),
+    so the reference returns np.average(samples, weights=None).  Iteration 0
+    (weights = ones) evaluates the same statistics up to rounding, so the window
+    is the rounding gap between the two top eigenvalues: found by bisection on
+    the reference's own outcome; None if that gap has the wrong sign."""
+    def outcome(sigma):
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                out = ref.ex_noregret(xs, eps, sigma, expansion, itv)
+        except TypeError:
+            return "typeerror", None
+        return "value", out
+    lo, hi = 1e-12, 10.0            # lo: TypeError, hi: exit at iteration 0
+    if outcome(lo)[0] != "typeerror" or outcome(hi)[0] != "value":
+        return None
+    for _ in range(200):
+        mid = np.sqrt(lo * hi) if hi / lo > 1.0 + 1e-9 else 0.5 * (lo + hi)
+        if mid in (lo, hi):
+            break
+        if outcome(mid)[0] == "typeerror":
+            lo = mid
+        else:
+            hi = mid
+    # hi is the smallest sigma (to the bisection's resolution) that returns; it
+    # exits at iteration 1 iff the result is the fp32 (unweighted) mean
+    # (a weighted fp64 average is practically never fp32-exact on every coordinate)
+    res = outcome(hi)[1]
+    if res is None or not np.all(np.asarray(res, np.float64) == np.asarray(res, np.float32)):
+        return None
+    return hi
+
+
+def degenerate_cases(ref):
+    """Round 4: the reference's behaviour on degenerate inputs.
+      * krum with NaN / inf clients: the NaN distances sort last (argsort), a
+        NaN score is np.argmin's answer (the FIRST NaN), inf - inf = NaN;
+      * bulyan(..., 'median') with a NaN client: every distance to the NaN
+        median is NaN, no strict minimum -> AssertionError (:308);
+        trimmedmean / krum modes with the same client;
+      * ex_noregret with an infeasible capped-simplex projection (cap
+        1/((1-eps) n') >= 1 -> break at i = 0, projected_c = None, :78-99):
+        TypeError at the next multiplicative update (:75), or -- when the next
+        iteration (weights=None) exits early -- the unweighted mean (:71-72)."""
+    out = []
+    xs = make_clients(12, (30,), 90)
+    xs[5][7] = np.nan
+    out.append(("krum_nan_client_n12_f2", "krum", {"f": 2}, xs, (lambda xs=xs: ref.krum(xs, 2))))
+    out.append(("krum__nan_client_n12_f2", "krum_", {"f": 2}, xs, (lambda xs=xs: ref.krum_(xs, 2))))
+    xs = make_clients(12, (30,), 91)
+    xs[8][1] = np.nan
+    xs[3][20] = np.nan
+    out.append(("krum_nan_two_n12_f2", "krum", {"f": 2}, xs, (lambda xs=xs: ref.krum(xs, 2))))
+    xs = make_clients(12, (30,), 92)
+    xs[2][3] = np.inf
+    xs[9][3] = np.inf           # inf - inf = NaN: d(2, 9) is NaN, d(2 or 9, others) inf
+    xs[4][10] = -np.inf
+    out.append(("krum_inf_clients_n12_f2", "krum", {"f": 2}, xs, (lambda xs=xs: ref.krum(xs, 2))))
+    out.append(("krum__inf_clients_n12_f2", "krum_", {"f": 2}, xs, (lambda xs=xs: ref.krum_(xs, 2))))
+    xs = make_clients(128, (300,), 93, byz=20)
+    xs[77][150] = np.nan
+    out.append(("krum_nan_client_n128_f20", "krum", {"f": 20}, xs, (lambda xs=xs: ref.krum(xs, 20))))
+    xs = make_clients(300, (64,), 94, byz=30)
+    xs[211][5] = np.nan
+    out.append(("krum_nan_client_n300_f30", "krum", {"f": 30}, xs, (lambda xs=xs: ref.krum(xs, 30))))
+    xs = make_clients(30, (40,), 95, byz=3)
+    xs[10][4] = np.nan
+    out.append(("mom_krum_nan_client_n30_f3", "mom_krum", {"f": 3}, xs, (lambda xs=xs: ref.mom_krum(xs, 3))))
+    xs = make_clients(24, (40,), 96, byz=5)
+    xs[7][13] = np.nan
+    for mode in ("median", "trimmedmean", "krum"):
+        out.append(("bulyan_%s_nan_client_n24_f5" % mode, "bulyan", {"f": 5, "aggsubfunc": mode}, xs,
+                    (lambda xs=xs, mode=mode: ref.bulyan(xs, 5, aggsubfunc=mode))))
+    xs = make_clients(24, (40,), 97, byz=5)
+    xs[11][2] = np.inf
+    out.append(("bulyan_median_inf_client_n24_f5", "bulyan", {"f": 5, "aggsubfunc": "median"}, xs,
+                (lambda xs=xs: ref.bulyan(xs, 5, aggsubfunc="median"))))
+    # ex_noregret, eps = 0.5, n = 4: f = 2, n' = 2, T = int(2 eps n') = 2,
+    # cap = 1/((1 - 0.5) 2) = 1 -> clip_norm = 0 -> projected_c = None at iteration 0
+    pn = {"eps": 0.5, "sigma": 1e-5, "expansion": 20, "itv": 20}
+    xs = make_clients(4, (20,), 98)
+    out.append(("ex_noregret_none_typeerror", "ex_noregret", pn, xs,
+                (lambda xs=xs, p=pn: ref.ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+    for seed in range(99, 160):
+        xs = make_clients(4, (20,), seed)
+        sig = _none_exit_sigma(ref, xs, 0.5, 20, 20)
+        if sig is not None:
+            pe = {"eps": 0.5, "sigma": float(sig), "expansion": 20, "itv": 20}
+            out.append(("ex_noregret_none_exit", "ex_noregret", pe, xs,
+                        (lambda xs=xs, p=pe: ref.ex_noregret(xs, p["eps"], p["sigma"], p["expansion"], p["itv"]))))
+            break
+    return out
+
+
 def main():
     ref = load_reference()
     cases = []
@@ -189,6 +286,8 @@ def main():
     cases.append(("mom_filterL2_n512_c5", "mom_filterL2", pc5, xs,
                   (lambda xs=xs, p=pc5: ref.mom_filterL2(xs, p["eps"], p["sigma"], p["expansion"], p["itv"],
                                                          p["delta"]))))
+
+    cases += degenerate_cases(ref)
 
     for name, func, params, xs, call in cases:
         if only and not any(o in name for o in only):

@@ -41,7 +41,8 @@ def test_oracle_matches_reference(rec):
     xs = [rec["x"][i] for i in range(rec["x"].shape[0])]
     call = CALL[rec["func"]]
     if "error" in rec:
-        exc = {"IndexError": IndexError, "ValueError": ValueError, "TypeError": TypeError}[rec["error"]]
+        exc = {"IndexError": IndexError, "ValueError": ValueError, "TypeError": TypeError,
+               "AssertionError": AssertionError}[rec["error"]]
         with pytest.raises(exc), warnings.catch_warnings():
             warnings.simplefilter("ignore")
             call(xs, rec["params"])
@@ -55,7 +56,9 @@ def test_oracle_matches_reference(rec):
     got = np.asarray(got)
     want = rec["out"]
     assert got.shape == want.shape
-    if rec["func"] in EXACT:
+    if rec["func"] in EXACT or rec["name"] == "ex_noregret_none_exit":
+        # (ex_noregret_none_exit: the reference's projection is infeasible and the
+        # next, unweighted iteration exits early with the fp32 mean, :65-72, 99)
         np.testing.assert_array_equal(got, want)
         if rec["func"] != "krum_":
             assert got.dtype == want.dtype
