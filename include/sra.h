@@ -213,9 +213,13 @@ int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes)
  * is filtered in client space from its centred fp64-MFMA Gram (top eigenpair
  * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 512 (n > 128: the
  * Gram in global memory, a 1024-thread re-orthogonalising solver per chunk).
- * status: device int32, zeroed by the caller; set to 2 when an ex_noregret
- * projection has no feasible candidate (the reference then fails with
- * TypeError).  ex_noregret with ceil(eps*n) = 0 or fewer than 2 clients left
+ * status: two device int32, zeroed by the caller.  ex_noregret whose
+ * capped-simplex projection has no feasible candidate (projected_c = None,
+ * robust_estimator.py:99) continues like the reference: the next iteration
+ * uses weights=None; status[0] = 2 when that iteration does not exit early
+ * (the reference then fails with TypeError at :75); otherwise -- or when it
+ * happens at the last iteration (:101) -- the chunk's result is the plain fp32
+ * mean of the kept clients, and status[1] counts such chunks.  ex_noregret with ceil(eps*n) = 0 or fewer than 2 clients left
  * after the Krum pre-filter -> SRA_ERR_ARG (the reference raises ValueError). */
 int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv, double eps,
                    double sigma, double expansion, double* out, int32_t* status, void* ws, size_t ws_bytes,

@@ -29,9 +29,10 @@ constexpr int kMaxClients = 512;
 // distance matrix (fp32) from the fp64 Gram.  A non-finite diagonal entry
 // means a NaN / inf somewhere in the data (the centring spreads it over every
 // entry): *nonfinite is set and the exact per-pair route below takes over.
-// acc (n x n fp64, optional) is zeroed for that route.
+// acc (n x n fp64) and cls (n x n int32 class bits), optional, are zeroed for
+// that route.
 __global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __restrict__ D, int* __restrict__ nonfinite,
-                                 double* __restrict__ acc) {
+                                 double* __restrict__ acc, int* __restrict__ cls) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n * n) return;
   const int i = e / n, j = e - (e / n) * n;
@@ -42,7 +43,10 @@ __global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __r
   }
   // a squared distance near fp32's range: the reference's fp32 norm overflows
   if (nonfinite != nullptr && sq > 3.0e38) atomicOr(nonfinite, 1);
-  if (acc != nullptr) acc[e] = 0.0;
+  if (acc != nullptr) {
+    acc[e] = 0.0;
+    cls[e] = 0;
+  }
   D[e] = static_cast<float>(sqrt(sq > 0.0 ? sq : 0.0));
 }
 
@@ -53,12 +57,16 @@ __global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __r
 // arithmetic reproduces; the pair's fp32 distance is sqrt(fp32(acc)).  Runs
 // only when krum_dist_kernel flagged the Gram (every block exits at once
 // otherwise).  Grid: (32 x 32 row-tile pairs I <= J) x d-slices; each thread
-// owns 4 pairs of its tile pair, fp64 partials added atomically.
+// owns 4 pairs of its tile pair.  Finite fp64 partials are added atomically;
+// a NaN / inf partial only sets its pair's class bit (1 NaN, 2 inf) -- the
+// class of a sum of non-negative squares is NaN if any term is, else inf if
+// any term is -- so no special value ever goes through the float atomic.
 constexpr int kDirTile = 32;
 constexpr int kDirK = 64;
 __global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
                                                           const int* __restrict__ nonfinite,
-                                                          double* __restrict__ acc, int nslices) {
+                                                          double* __restrict__ acc, int* __restrict__ cls,
+                                                          int nslices) {
   if (*nonfinite == 0) return;
   __shared__ float ta[kDirTile][kDirK + 1];
   __shared__ float tb[kDirTile][kDirK + 1];
@@ -97,7 +105,12 @@ __global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restric
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = J * kDirTile + tj + q;
-    if (i < n && j < n && (I < J || i < j)) atomicAdd(&acc[static_cast<int64_t>(i) * n + j], s[q]);
+    if (i < n && j < n && (I < J || i < j)) {
+      const int64_t e = static_cast<int64_t>(i) * n + j;
+      if (s[q] != s[q]) atomicOr(&cls[e], 1);
+      else if (__builtin_isinf(s[q])) atomicOr(&cls[e], 2);
+      else if (s[q] != 0.0) atomicAdd(&acc[e], s[q]);
+    }
   }
 }
 
@@ -107,7 +120,8 @@ __global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restric
 __global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restrict__ D, int n,
                                                            float* __restrict__ S, int* __restrict__ J,
                                                            const int* __restrict__ nonfinite,
-                                                           const double* __restrict__ acc) {
+                                                           const double* __restrict__ acc,
+                                                           const int* __restrict__ cls) {
   __shared__ float kv[kMaxClients];
   __shared__ int kj[kMaxClients];
   const int i = blockIdx.x;
@@ -119,8 +133,10 @@ __global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restri
     if (p < m) {
       const int j = p < i ? p : p + 1;
       if (direct) {
-        const double sq = i < j ? acc[(int64_t)i * n + j] : acc[(int64_t)j * n + i];
-        kv[p] = sqrtf(static_cast<float>(sq));   // np.sqrt of the fp32 squared norm (inf on fp32 overflow)
+        const int64_t e = i < j ? (int64_t)i * n + j : (int64_t)j * n + i;
+        const int c = cls[e];
+        // np.sqrt of the fp32 squared norm (inf on fp32 overflow)
+        kv[p] = (c & 1) ? __builtin_nanf("") : (c & 2) ? __builtin_inff() : sqrtf(static_cast<float>(acc[e]));
       } else {
         kv[p] = D[(int64_t)i * n + j];
       }
@@ -139,9 +155,11 @@ __global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restri
         const bool up = (a & k) == 0;
         const float va = kv[a], vb = kv[b];
         const int ja = kj[a], jb = kj[b];
-        // order (value, j); NaN sorts as the largest value
-        const bool a_gt = (va != va) ? !((vb != vb) && ja < jb)
-                                     : ((vb != vb) ? false : (va > vb || (va == vb && ja > jb)));
+        // order (class, value, j): numbers ascending (inf included), then NaN
+        // (argsort's NaN-last), then the padding slots (j = INT_MAX)
+        const int ca = ja == 0x7fffffff ? 2 : (va != va ? 1 : 0);
+        const int cb = jb == 0x7fffffff ? 2 : (vb != vb ? 1 : 0);
+        const bool a_gt = ca != cb ? ca > cb : (ca == 0 ? (va > vb || (va == vb && ja > jb)) : ja > jb);
         if (a_gt == up) {
           kv[a] = vb; kv[b] = va;
           kj[a] = jb; kj[b] = ja;
@@ -365,24 +383,25 @@ size_t krum_workspace_bytes(int n, int64_t d);
 size_t gram_workspace_bytes(int n, int64_t d);
 int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes, hipStream_t s);
 
-// workspace layout: [flag (256 B)][G fp64 n*n][acc fp64 n*n][D n*n][S n*n][J n*n][gram slab]
+// workspace layout: [flag (256 B)][G fp64 n*n][acc fp64 n*n][cls int n*n][D n*n][S n*n][J n*n][gram slab]
 size_t krum_workspace_bytes(int n, int64_t d) {
   const size_t nn = static_cast<size_t>(n) * n;
-  return 256 + nn * 8 * 2 + nn * 4 * 3 + gram_workspace_bytes(n, d);
+  return 256 + nn * 8 * 2 + nn * 4 * 4 + gram_workspace_bytes(n, d);
 }
 
 // X (optional): the data G came from; with it, a non-finite G switches the
 // distances to the exact per-pair route (krum_direct_kernel), nonfinite / acc
 // its flag and n x n fp64 accumulator
 static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* order, float* scores0, char* ws,
-                              const float* X, int64_t d, int64_t ldx, int* nonfinite, double* acc, hipStream_t s) {
+                              const float* X, int64_t d, int64_t ldx, int* nonfinite, double* acc, int* cls,
+                              hipStream_t s) {
   const size_t nn = static_cast<size_t>(n) * n;
   float* D = reinterpret_cast<float*>(ws);
   float* S = D + nn;
   int* J = reinterpret_cast<int*>(S + nn);
   if (X != nullptr) SRA_HIP(hipMemsetAsync(nonfinite, 0, sizeof(int), s));
   hipLaunchKernelGGL(krum_dist_kernel, dim3(cdiv(n * n, 256)), dim3(256), 0, s, G, n, D, X ? nonfinite : nullptr,
-                     X ? acc : nullptr);
+                     X ? acc : nullptr, X ? cls : nullptr);
   int rc = launch_status("krum_dist_kernel");
   if (rc) return rc;
   if (X != nullptr && n > 1) {
@@ -390,13 +409,13 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
     const int64_t kb = cdiv(d, kDirK);
     const int slices = static_cast<int>(kb < 256 ? kb : 256);
     hipLaunchKernelGGL(krum_direct_kernel, dim3(slices, nt * (nt + 1) / 2), dim3(256), 0, s, X, n, d, ldx,
-                       nonfinite, acc, slices);
+                       nonfinite, acc, cls, slices);
     rc = launch_status("krum_direct_kernel");
     if (rc) return rc;
   }
   if (n > 1) {
     hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), 0, s, D, n, S, J, X ? nonfinite : nullptr,
-                       X ? acc : nullptr);
+                       X ? acc : nullptr, X ? cls : nullptr);
     rc = launch_status("krum_rowsort_kernel");
     if (rc) return rc;
   }
@@ -435,7 +454,7 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
 
 int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int* order, float* scores0,
                                  char* ws, hipStream_t s) {
-  return launch_krum_rounds(G, n, f, rounds, order, scores0, ws, nullptr, 0, 0, nullptr, nullptr, s);
+  return launch_krum_rounds(G, n, f, rounds, order, scores0, ws, nullptr, 0, 0, nullptr, nullptr, nullptr, s);
 }
 
 int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds, int* order, float* scores0,
@@ -449,11 +468,12 @@ int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds
   int* nonfinite = reinterpret_cast<int*>(base);
   double* G = reinterpret_cast<double*>(base + 256);
   double* acc = G + nn;
-  char* rest = reinterpret_cast<char*>(acc + nn);
+  int* cls = reinterpret_cast<int*>(acc + nn);
+  char* rest = reinterpret_cast<char*>(cls + nn);
   char* slab = rest + nn * 4 * 3;
   int rc = launch_gram(X, n, d, ldx, G, slab, gram_workspace_bytes(n, d), s);
   if (rc) return rc;
-  return launch_krum_rounds(G, n, f, rounds, order, scores0, rest, X, d, ldx, nonfinite, acc, s);
+  return launch_krum_rounds(G, n, f, rounds, order, scores0, rest, X, d, ldx, nonfinite, acc, cls, s);
 }
 
 }  // namespace sra

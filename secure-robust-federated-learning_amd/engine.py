@@ -268,20 +268,31 @@ def chunk_width(d, itv):
     return int(itv)
 
 
-def _filter(X, mode, eps, sigma, expansion, itv, check, out=None):
+def _filter(X, mode, eps, sigma, expansion, itv, check, out=None, info=None):
+    """info (a dict, optional): ``unweighted_chunks`` = the chunks whose result
+    is ex_noregret's plain fp32 mean after an infeasible projection
+    (projected_c = None, robust_estimator.py:99-101), ``chunks`` = all chunks
+    (one host synchronisation)."""
     X, n, d, ldx = as_matrix(X)
     if out is None:
         out = torch.empty(d, dtype=torch.float64, device=X.device)
     elif out.dtype != torch.float64 or out.numel() != d or not out.is_contiguous() or out.device != X.device:
         raise ValueError("out must be a contiguous float64 (d,) tensor on X's device")
-    status = torch.zeros(1, dtype=torch.int32, device=X.device)
+    status = torch.zeros(2, dtype=torch.int32, device=X.device)
     w = chunk_width(d, itv)
     nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
     ws = _workspace(nb, X.device)
     _lib.call("sra_filter_f32", X.data_ptr(), n, d, ldx, int(mode), w, float(eps), float(sigma),
               float(expansion), out.data_ptr(), status.data_ptr(), ws.data_ptr(), nb, _stream_ptr(X.device))
-    if check and int(status.item()) == 2:
-        raise TypeError("ex_noregret: no feasible capped-simplex projection (projected_c is None)")
+    if check or info is not None:
+        st = status.cpu().tolist()
+        if check and st[0] == 2:
+            raise TypeError("ex_noregret: no feasible capped-simplex projection (projected_c is None), and the "
+                            "next (unweighted) iteration does not exit: unsupported operand type(s) for *: "
+                            "'NoneType' and 'float'")
+        if info is not None:
+            info["unweighted_chunks"] = int(st[1])
+            info["chunks"] = -(-d // w)
     return out
 
 
@@ -295,7 +306,7 @@ def filter_trace(X, mode, eps, sigma, expansion, itv):
     of oracle.robust_np.trace_array (sra_filter_trace_f32, include/sra.h)."""
     X, n, d, ldx = as_matrix(X)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
-    status = torch.zeros(1, dtype=torch.int32, device=X.device)
+    status = torch.zeros(2, dtype=torch.int32, device=X.device)
     w = chunk_width(d, itv)
     nch = -(-d // w)
     half = max(n, 128)   # rows of 1 + 2 max(N, 128) int32 (include/sra.h)
@@ -319,7 +330,7 @@ def filter_debug(X, mode, eps, sigma, expansion, itv):
     second_gs_passes, cycles, 7 unused]."""
     X, n, d, ldx = as_matrix(X)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
-    status = torch.zeros(1, dtype=torch.int32, device=X.device)
+    status = torch.zeros(2, dtype=torch.int32, device=X.device)
     dbg = torch.full((FILTER_DEBUG_DOUBLES,), float("nan"), dtype=torch.float64, device=X.device)
     w = chunk_width(d, itv)
     nb = _lib.query_bytes("sra_filter_workspace_bytes", n, d, w)
@@ -338,9 +349,9 @@ def filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, check=True, out=None):
     return _filter(X, 0, eps, sigma, expansion, itv, check, out)
 
 
-def ex_noregret(X, eps=1. / 12, sigma=1, expansion=20, itv=ITV, check=True, out=None):
+def ex_noregret(X, eps=1. / 12, sigma=1, expansion=20, itv=ITV, check=True, out=None, info=None):
     """robust_estimator.ex_noregret on device: float64 (d,) (into ``out`` when given)."""
-    return _filter(X, 1, eps, sigma, expansion, itv, check, out)
+    return _filter(X, 1, eps, sigma, expansion, itv, check, out, info)
 
 
 def mom_bucket_count(n, eps, delta):
@@ -361,10 +372,10 @@ def mom_filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.7182818284
 
 
 def mom_ex_noregret(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True,
-                    out=None):
+                    out=None, info=None):
     n = int(X.shape[0])
     num, size = mom_bucket_count(n, eps, delta)
-    return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check, out)
+    return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check, out, info)
 
 
 # ---------------------------------------------------------------------------

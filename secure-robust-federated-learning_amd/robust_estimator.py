@@ -201,20 +201,34 @@ def mom_filterL2(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(
     return st.result(engine.mom_filter_l2(st.X, eps, sigma, expansion, itv, delta), dtype=np.float64)
 
 
+def _noregret_dtype(info):
+    """The reference's result dtype: every chunk float64 (np.average with
+    weights), except that a chunk whose projection was infeasible returns the
+    plain float32 mean (robust_estimator.py:65, 101) -- np.concatenate keeps
+    float32 only when every chunk did."""
+    return np.float32 if info["chunks"] and info["unweighted_chunks"] == info["chunks"] else np.float64
+
+
 def ex_noregret_(samples, eps=1. / 12, sigma=1, expansion=20, dis_threshold=0.7):
     """robust_estimator.py:42-102 on one (n, k) chunk."""
     st = _stage(samples)
     k = int(st.X.shape[1])
-    return st.result(engine.ex_noregret(st.X, eps, sigma, expansion, itv=k), dtype=np.float64)
+    info = {}
+    out = engine.ex_noregret(st.X, eps, sigma, expansion, itv=k, info=info)
+    return st.result(out, dtype=_noregret_dtype(info))
 
 
 def ex_noregret(samples, eps=1. / 12, sigma=1, expansion=20, itv=ITV):
     """robust_estimator.py:104-133."""
     st = _stage(samples)
-    return st.result(engine.ex_noregret(st.X, eps, sigma, expansion, itv), dtype=np.float64)
+    info = {}
+    out = engine.ex_noregret(st.X, eps, sigma, expansion, itv, info=info)
+    return st.result(out, dtype=_noregret_dtype(info))
 
 
 def mom_ex_noregret(samples, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=np.exp(-30)):
     """robust_estimator.py:135-142."""
     st = _stage(samples)
-    return st.result(engine.mom_ex_noregret(st.X, eps, sigma, expansion, itv, delta), dtype=np.float64)
+    info = {}
+    out = engine.mom_ex_noregret(st.X, eps, sigma, expansion, itv, delta, info=info)
+    return st.result(out, dtype=_noregret_dtype(info))
