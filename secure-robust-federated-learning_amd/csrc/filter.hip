@@ -2105,389 +2105,6 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
   }
 }
 
-// ---- lanczos_cb_kernel (round 4): filterL2 on the column-block layout -----
-// One 256-thread workgroup per chunk (two per CU), a work queue of chunks.
-// Wave w holds the column block G[:, 32w .. 32w + 31] of the chunk Gram (lane
-// l: rows l and l + 64, 64 doubles), and EVERY wave holds every client-space
-// vector (rows l and l + 64 per lane) and computes every dot product itself, so
-// a Lanczos step has ONE workgroup barrier: the exchange of the four waves'
-// partial products G[:, block] x[block].  M = W^1/2 C W^1/2 is applied
-// implicitly from the fixed G (C x' = G x' - g (1.x') - 1 (g.x') + s 1 (1.x'),
-// g = G w, s = w.g), so G is loaded once per chunk, not once per iteration.
-// The Lanczos basis is not stored: the Ritz vector u = V z of an accepted
-// check is assembled by replaying the recurrence (the same operations on the
-// same values: bitwise the same q_j) with the recorded alpha / beta.  Checks:
-// fast_check (block-wide).  A chunk whose top pair plain Lanczos cannot
-// resolve (a ghost after the dense-check retry, or MMAX steps) is listed for
-// filter_solve_kernel<0> (re-orthogonalising), which redoes it.
-// out of line: the check's registers must not compete with the 64 Gram values
-// per lane of the Lanczos step
-__device__ __attribute__((noinline)) void fast_check_ol(const double* T, int m, double theta_lb, double hint,
-                                                        double glo, double ghi, double* z, double* scr,
-                                                        double* theta_out, double* zlast_out, int* rounds_out) {
-  fast_check(T, m, theta_lb, hint, glo, ghi, z, scr, theta_out, zlast_out, rounds_out);
-}
-
-constexpr size_t kCbLds = sizeof(double) * (2 * 4 * FNP + 4 * FNP + kTrw + 2 * MMAX + kCheckScr + 16 + FNP + 240) +
-                          sizeof(int) * (16 + FNP);
-static_assert(2 * kCbLds <= 163840, "two column-block workgroups must fit one CU's LDS");
-
-template <bool DBG>
-__global__ void __launch_bounds__(256, 2) lanczos_cb_kernel(SolveArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* part = reinterpret_cast<double*>(smem);   // [2][4][FNP] matvec partials (step parity)
-  double* xsb = part + 2 * 4 * FNP;                 // [4][FNP] each wave's own copy of the operator input
-  double* trw = xsb + 4 * FNP;                      // [kTrw] tridiagonal record (wave 0 writes)
-  double* zbuf = trw + kTrw;                        // [2][MMAX] eigenvectors of T (current / best check)
-  double* cscr = zbuf + 2 * MMAX;                   // [kCheckScr] check scratch
-  double* misc = cscr + kCheckScr;                  // [16]
-  double* cvec = misc + 16;                         // [FNP] final weights (the np.average scale)
-  double* clog = cvec + FNP;                        // [60][4] DBG: check log
-  int* qslot = reinterpret_cast<int*>(clog + 240);  // [16]
-  int* aflag = qslot + 16;                          // [FNP] final active flags
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int n = A.n;
-  const int r0 = lane, r1 = lane + 64;   // this lane's two client rows
-  double* xw = xsb + wave * FNP;
-  if (tid < 16) trw[2 * MMAX + tid] = 0.0;   // prefetch padding of the T record
-
-  // sum over both rows of every lane, identical in every wave (no barrier)
-  auto vsum = [&](double a0, double a1) __attribute__((always_inline)) -> double { return wave_sum(a0 + a1); };
-
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) *qslot = atomicAdd(A.fb_count + 4, 1);
-    __syncthreads();
-    const int ch = *qslot;
-    if (ch >= A.nb) break;
-    // ---- G's column block into registers: g[c] = G[r0][32w + c], g[32 + c] = G[r1][32w + c]
-    double g[64];
-    {
-      const double* Gc = A.G + static_cast<size_t>(ch) * FNP * FNP + 32 * wave;
-      const double2* g0 = reinterpret_cast<const double2*>(Gc + static_cast<size_t>(r0) * FNP);
-      const double2* g1 = reinterpret_cast<const double2*>(Gc + static_cast<size_t>(r1) * FNP);
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double2 a = g0[c], b = g1[c];
-        g[2 * c] = a.x;
-        g[2 * c + 1] = a.y;
-        g[32 + 2 * c] = b.x;
-        g[32 + 2 * c + 1] = b.y;
-      }
-    }
-    int par = 0;
-    // (y0, y1) = G x' over the whole chunk for x' given per row: this wave's
-    // column block from its own LDS copy (broadcast reads), the four waves'
-    // partials exchanged behind one barrier and summed in wave order
-    auto graw = [&](double x0, double x1, double& y0, double& y1) __attribute__((always_inline)) {
-      xw[r0] = x0;
-      xw[r1] = x1;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const double2* xb = reinterpret_cast<const double2*>(xw + 32 * wave);
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-#pragma unroll
-      for (int c = 0; c < 16; c += 2) {
-        const double2 a = xb[c], b = xb[c + 1];
-        p0 = fma(g[2 * c], a.x, p0);
-        p1 = fma(g[2 * c + 1], a.y, p1);
-        p0 = fma(g[2 * c + 2], b.x, p0);
-        p1 = fma(g[2 * c + 3], b.y, p1);
-        p2 = fma(g[32 + 2 * c], a.x, p2);
-        p3 = fma(g[32 + 2 * c + 1], a.y, p3);
-        p2 = fma(g[32 + 2 * c + 2], b.x, p2);
-        p3 = fma(g[32 + 2 * c + 3], b.y, p3);
-        // at most 8 x pieces in flight (the compiler would hoist all 32 reads)
-        if ((c & 6) == 6) asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3)::"memory");
-      }
-      double* P = part + par * 4 * FNP;
-      P[wave * FNP + r0] = p0 + p1;
-      P[wave * FNP + r1] = p2 + p3;
-      lds_barrier();
-      y0 = ((P[r0] + P[FNP + r0]) + P[2 * FNP + r0]) + P[3 * FNP + r0];
-      y1 = ((P[r1] + P[FNP + r1]) + P[2 * FNP + r1]) + P[3 * FNP + r1];
-      par ^= 1;
-    };
-
-    const bool dbg = DBG && ch == 0;
-    bool a0 = r0 < n, a1 = r1 < n;   // active clients
-    double c0 = a0 ? 1.0 : 0.0, c1 = a1 ? 1.0 : 0.0;
-    const int iters = 2 * static_cast<int>(A.eps * n);
-    int m_hint = 24;
-    double rate_hint = 0.0;
-    bool fallback = false;
-    int clog_n = 0;
-    int done = 0;
-    int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
-
-    for (int it = 0; it < iters; ++it) {
-      const long long t_it = dbg ? clock64() : 0;
-      if (DBG) clog_n = 0;
-      // ---- weights, g = G w, s = w.g
-      const double csum = vsum(a0 ? c0 : 0.0, a1 ? c1 : 0.0);
-      const int nact = static_cast<int>(vsum(a0 ? 1.0 : 0.0, a1 ? 1.0 : 0.0));
-      const double w0 = a0 ? c0 / csum : 0.0, w1 = a1 ? c1 / csum : 0.0;
-      const double sw0 = sqrt(w0 > 0.0 ? w0 : 0.0), sw1 = sqrt(w1 > 0.0 ? w1 : 0.0);
-      double gv0, gv1;
-      graw(w0, w1, gv0, gv1);
-      const double sgw = vsum(w0 * gv0, w1 * gv1);
-      // (y0, y1) = M x = W^1/2 C W^1/2 x
-      auto mv = [&](double x0, double x1, double& y0, double& y1) __attribute__((always_inline)) {
-        const double xs0 = sw0 * x0, xs1 = sw1 * x1;
-        const double sa = vsum(xs0, xs1);
-        const double sb = vsum(gv0 * xs0, gv1 * xs1);
-        double t0, t1;
-        graw(xs0, xs1, t0, t1);
-        const double k1 = sgw * sa - sb;
-        y0 = sw0 * ((t0 - gv0 * sa) + k1);
-        y1 = sw1 * ((t1 - gv1 * sa) + k1);
-      };
-
-      // ---- top eigenpair of M by plain Lanczos; checks by fast_check, the
-      // best residual kept, a ghost retries once with dense checks
-      double lam = 0.0, resid = 0.0, u0 = 0.0, u1 = 0.0;
-      int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
-      bool converged = false;
-      double tscale = 0.0;
-      long long tcheck = 0;
-      int trounds = 0;
-      const double s0h = 0.5 + (r0 * 0.6180339887498949 - floor(r0 * 0.6180339887498949));
-      const double s1h = 0.5 + (r1 * 0.6180339887498949 - floor(r1 * 0.6180339887498949));
-      const double st0 = sw0 > 0.0 ? sw0 * s0h : 0.0, st1 = sw1 > 0.0 ? sw1 * s1h : 0.0;
-      const double nrm2_0 = vsum(st0 * st0, st1 * st1);
-      for (int attempt = 0; attempt < 2 && !converged; ++attempt) {
-        double x0 = st0, x1 = st1, nrm2 = nrm2_0;
-        double qp0 = 0.0, qp1 = 0.0, theta_lb = -1e300, hint = -1.0;
-        double res_best = 1e300, lam_best = 0.0;
-        tscale = 0.0;
-        double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
-        const int adv_max = attempt == 1 ? 1 : A.max_adv;
-        const int first = m_hint + A.first_off > 4 ? m_hint + A.first_off : 4;
-        int next_check = attempt == 1 ? (m_retry > 4 ? m_retry : 4) : first;
-        int m_a = -1, m_last = 4, m_pre = 4;
-        double res_a = 0.0;
-        bool ghost = false;
-        for (int j = 0;; ++j) {
-          const double bet = sqrt(nrm2);
-          if (j > 0) {
-            if (tid == 0) trw[2 * j + 1] = nrm2;
-            tscale = fmax(tscale, bet);
-            const bool breakdown = !(bet > 1e-14 * tscale);
-            if (breakdown || j == MMAX || j >= next_check) {
-              const int m = j;
-              ++nchecks;
-              const long long tc0 = dbg ? clock64() : 0;
-              double lm, zl;
-              int rounds = 0;
-              const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
-              lds_barrier();   // the record's last entries (wave 0) before every wave reads it
-              fast_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, cscr, &lm, &zl, &rounds);
-              if (dbg) {
-                tcheck += clock64() - tc0;
-                trounds += rounds;
-              }
-              const double res = fabs(bet * zl);
-              if (DBG && tid == 0 && clog_n < 60) {
-                double* lg = clog + 4 * clog_n;
-                lg[0] = m + 1000.0 * attempt + 10000.0 * it;
-                lg[1] = lm;
-                lg[2] = zl;
-                lg[3] = bet;
-              }
-              ++clog_n;
-              hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
-              theta_lb = lm;
-              if (res <= kAccept * fabs(lm) || breakdown) {
-                converged = true;
-                m_conv = m;
-                lam = lm;
-                resid = res;
-                zbest = zcur;
-                break;
-              }
-              if (res < res_best) {
-                m_pre = m_last;
-                res_best = res;
-                lam_best = lm;
-                zbest = zcur;
-                zcur ^= 1;
-              }
-              ghost = res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
-              const bool out_of_steps = j == MMAX;
-              if (ghost || out_of_steps) {
-                if (tid == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
-                if (!ghost) attempt = 1;   // out of steps: no retry helps
-                m_retry = m_pre;
-                ghost = true;
-                break;
-              }
-              int adv = 4;
-              double rate = rate_hint;
-              if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
-              if (rate < 0.0 && res > 0.0) {
-                const double need = log(kAccept * fabs(lm) / res) / rate;
-                adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
-              }
-              m_a = m;
-              res_a = res;
-              m_last = m;
-              next_check = m + adv;
-            }
-            gfin_hi = fmax(gfin_hi, a_last + b_prev + bet);
-            gfin_lo = fmin(gfin_lo, a_last - b_prev - bet);
-            b_prev = bet;
-          }
-          double y0, y1;
-          mv(x0, x1, y0, y1);
-          const double ib = 1.0 / bet;
-          const double q0 = x0 * ib, q1 = x1 * ib;
-          const double mq0 = y0 * ib, mq1 = y1 * ib;
-          const double aj = vsum(q0 * mq0, q1 * mq1);
-          const double rn0 = mq0 - aj * q0 - (j > 0 ? bet * qp0 : 0.0);
-          const double rn1 = mq1 - aj * q1 - (j > 0 ? bet * qp1 : 0.0);
-          if (tid == 0) trw[2 * j] = aj;
-          a_last = aj;
-          tscale = fmax(tscale, fabs(aj));
-          qp0 = q0;
-          qp1 = q1;
-          x0 = rn0;
-          x1 = rn1;
-          nrm2 = vsum(rn0 * rn0, rn1 * rn1);
-        }
-        if (!ghost) break;
-      }
-      if (!converged) {
-        fallback = true;
-        break;
-      }
-      // ---- Ritz vector u = sum_j z_j q_j: replay the recurrence (the q_j are
-      // bitwise those of the first pass: same operations, alpha / beta^2 from
-      // the record)
-      lds_barrier();   // z of the accepted check (wave 0 wrote it) and the record
-      {
-        const double* zb = zbuf + zbest * MMAX;
-        double x0 = st0, x1 = st1, qp0 = 0.0, qp1 = 0.0;
-        double bet = sqrt(nrm2_0);
-        for (int j = 0; j < m_conv; ++j) {
-          const double ib = 1.0 / bet;
-          const double q0 = x0 * ib, q1 = x1 * ib;
-          const double zj = zb[j];
-          u0 = fma(zj, q0, u0);
-          u1 = fma(zj, q1, u1);
-          if (j + 1 == m_conv) break;
-          double y0, y1;
-          mv(x0, x1, y0, y1);
-          const double mq0 = y0 * ib, mq1 = y1 * ib;
-          const double aj = trw[2 * j];
-          const double rn0 = mq0 - aj * q0 - (j > 0 ? bet * qp0 : 0.0);
-          const double rn1 = mq1 - aj * q1 - (j > 0 ? bet * qp1 : 0.0);
-          qp0 = q0;
-          qp1 = q1;
-          x0 = rn0;
-          x1 = rn1;
-          bet = sqrt(trw[2 * (j + 1) + 1]);
-        }
-        if (sw0 == 0.0) u0 = 0.0;
-        if (sw1 == 0.0) u1 = 0.0;
-      }
-      m_hint = m_conv > 8 ? m_conv : 8;
-      if (dbg && it < 256) {
-        double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
-        if (wave == 0) {
-          rec[r0] = c0;
-          rec[r1] = c1;
-        }
-        if (tid == 0) {
-          rec[FNP] = lam;
-          rec[FNP + 1] = m_conv;
-          rec[FNP + 2] = resid;
-          rec[FNP + 3] = nchecks;
-          rec[FNP + 4] = nact;
-          rec[FNP + 5] = sgw;
-          rec[FNP + 6] = 0;
-          rec[FNP + 7] = 0;
-          rec[FNP + 8] = static_cast<double>(clock64() - t_it);
-          rec[FNP + 9] = static_cast<double>(tcheck);
-          rec[FNP + 10] = 0;
-          rec[FNP + 11] = 0;
-          rec[FNP + 12] = trounds;
-        }
-      }
-      // ---- early exit (robust_estimator.py:163-164)
-      if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
-      // ---- tau_i = ((M u)_i / sqrt(w_i))^2 / lambda; drop the first argmax
-      double mu0, mu1;
-      mv(u0, u1, mu0, mu1);
-      const double cu0 = sw0 > 0.0 ? mu0 / sw0 : 0.0, cu1 = sw1 > 0.0 ? mu1 / sw1 : 0.0;
-      const double t0 = cu0 * cu0 / lam, t1 = cu1 * cu1 / lam;
-      double bv = a0 ? t0 : -__builtin_inf();
-      int bi = r0;
-      if (a1 && t1 > bv) {   // r1 > r0: a tie keeps r0
-        bv = t1;
-        bi = r1;
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const double ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
-        if (ov > bv || (ov == bv && oi < bi)) {
-          bv = ov;
-          bi = oi;
-        }
-      }
-      const int p = __builtin_amdgcn_readfirstlane(bi);
-      const double tmax = readlane_f64(bv, 0);
-      const double cn0 = (a0 && r0 != p) ? c0 * (1.0 - t0 / tmax) : 0.0;
-      const double cn1 = (a1 && r1 != p) ? c1 * (1.0 - t1 / tmax) : 0.0;
-      const double cs = vsum(fabs(cn0), fabs(cn1));
-      c0 = cn0 / cs;
-      c1 = cn1 / cs;
-      if (r0 == p) a0 = false;
-      if (r1 == p) a1 = false;
-      if (tr != nullptr && tid == 0) tr[1 + it] = p;
-      done = it + 1;
-    }
-
-    if (fallback) {
-      if (tid == 0) {
-        const int k = atomicAdd(A.fb_count, 1);
-        A.fb_list[k] = ch;
-        if (DBG && k == 0 && A.dbg != nullptr) {
-          double* lg = A.dbg + FNP * FNP + 250 * kDbgRec;
-          for (int e = 0; e < 4 * (clog_n < 60 ? clog_n : 60); ++e) lg[e] = clog[e];
-        }
-      }
-      continue;
-    }
-    if (wave == 0) {
-      cvec[r0] = a0 ? c0 : 0.0;
-      cvec[r1] = a1 ? c1 : 0.0;
-      aflag[r0] = a0 ? 1 : 0;
-      aflag[r1] = a1 ? 1 : 0;
-      A.c[static_cast<size_t>(ch) * FNP + r0] = a0 ? c0 : 0.0;
-      A.c[static_cast<size_t>(ch) * FNP + r1] = a1 ? c1 : 0.0;
-      A.act[static_cast<size_t>(ch) * FNP + r0] = a0 ? 1 : 0;
-      A.act[static_cast<size_t>(ch) * FNP + r1] = a1 ? 1 : 0;
-      if (tr != nullptr) {
-        tr[1 + FNP + r0] = a0 ? 1 : 0;
-        tr[1 + FNP + r1] = a1 ? 1 : 0;
-      }
-    }
-    if (tr != nullptr && tid == 0) tr[0] = done;
-    lds_barrier();
-    if (tid == 0) {
-      // np.average's scale: numpy's pairwise sum of the kept weights in client order
-      int q2 = 0;
-      double* kept = cscr;
-      for (int i = 0; i < n; ++i)
-        if (aflag[i]) kept[q2++] = cvec[i];
-      A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
-    }
-  }
-}
-
 __global__ void list_all_kernel(int* list, int* count, int nb) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < nb) list[i] = i;
@@ -3173,15 +2790,15 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(lgrid_max) * MMAX * FNP);
   int* fbl = aws + static_cast<size_t>(bmax) * FNP;
   int* fbc = fbl + bmax;   // [0] listed chunks, [1] ghost after the retry, [2] out of steps, [3] retries,
-                           // [4] lanczos_solve_kernel's chunk queue
+                           // [4] the solver's chunk queue
   const void* solve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<0, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<0, false>))
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<1, false>));
   SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
-  const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_cb_kernel<true>)
-                           : reinterpret_cast<const void*>(&lanczos_cb_kernel<false>);
-  SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kCbLds)));
+  const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
+                           : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
+  SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLds)));
   // ex_noregret stays on the re-orthogonalising kernel: on the plain solver
   // (217 vs 327 ms at C4) every traced decision agreed, but the C4 fixture
   // chunk 1 landed 2.9e-3 of max from the reference (bound 2e-5) and two DBA
@@ -3217,9 +2834,9 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("list_all_kernel");
       if (rc) return rc;
     } else {
-      if (dbg) hipLaunchKernelGGL((lanczos_cb_kernel<true>), dim3(lgrid), dim3(256), kCbLds, s, sa);
-      else hipLaunchKernelGGL((lanczos_cb_kernel<false>), dim3(lgrid), dim3(256), kCbLds, s, sa);
-      rc = launch_status("lanczos_cb_kernel");
+      if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<0, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      else hipLaunchKernelGGL((lanczos_solve_kernel<0, false>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      rc = launch_status("lanczos_solve_kernel");
       if (rc) return rc;
     }
     // the listed chunks (not converged / ghost) on the re-orthogonalising solver
@@ -3233,7 +2850,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     // diagnostics: the first batch's fallback count, as an int32 in the low
     // word of the last record's last slot
     if (dbg != nullptr && c0 == 0)
-      SRA_HIP(hipMemcpyAsync(dbg + FNP * FNP + 255 * kDbgRec + kDbgRec - 2, fbc, 4 * sizeof(int), hipMemcpyDeviceToDevice, s));
+      SRA_HIP(hipMemcpyAsync(dbg + FNP * FNP + 255 * kDbgRec + kDbgRec - 3, fbc, 6 * sizeof(int), hipMemcpyDeviceToDevice, s));
     const int64_t jend = (c0 + nb) * static_cast<int64_t>(itv);
     const int64_t ncols = (jend < d ? jend : d) - c0 * static_cast<int64_t>(itv);
     hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws,
