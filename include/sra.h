@@ -165,8 +165,8 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
  * columns.  Column shards' dist vectors sum to the full distance (up to fp64
  * rounding: the per-tile partials are associated differently).  N <= 512
  * (rounds with more than 128 listed rows take an LDS k-select + distance pass);
- * workspace from sra_bulyan_round_workspace_bytes. */
-int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes);
+ * workspace from sra_bulyan_round_workspace_bytes (sized by the block's d). */
+int sra_bulyan_round_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
 int sra_bulyan_round_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const int32_t* rows, int32_t nr,
                          int32_t mode, int32_t dba, float* agg, double* dist, void* ws, size_t ws_bytes,
                          void* stream);

@@ -76,7 +76,7 @@ _SIGS = {
     "sra_bulyan_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _ptr, _sz, _ptr],
     "sra_bulyan_coordinate_f64": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
     "sra_bulyan_stage_workspace_bytes": [_i64, _i64, ctypes.POINTER(_sz)],
-    "sra_bulyan_round_workspace_bytes": [_i64, ctypes.POINTER(_sz)],
+    "sra_bulyan_round_workspace_bytes": [_i64, _i64, ctypes.POINTER(_sz)],
     "sra_bulyan_round_f32": [_ptr, _i64, _i64, _i64, _ptr, _i32, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
     "sra_bulyan_pick": [_ptr, _ptr, _i32, _ptr, _ptr, _ptr],
     "sra_bulyan_stage_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr, _sz, _ptr],

@@ -1310,11 +1310,11 @@ extern "C" int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, in
 
 // One Bulyan selection round over a (possibly column-sharded) N x d block, for
 // a caller that sums the shards' distances (all-reduce) and picks itself.
-extern "C" int sra_bulyan_round_workspace_bytes(int64_t n, size_t* bytes) {
+extern "C" int sra_bulyan_round_workspace_bytes(int64_t n, int64_t d, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
-  SRA_REQUIRE(n >= 1 && n <= kBigMaxClients, SRA_ERR_UNSUPPORTED, "bulyan rounds support 1 <= N <= %d",
-              kBigMaxClients);
-  *bytes = sizeof(float) * static_cast<size_t>(n) * kRoundMaxBlocks + 256;
+  SRA_REQUIRE(n >= 1 && n <= kBigMaxClients && d >= 1, SRA_ERR_UNSUPPORTED,
+              "bulyan rounds support 1 <= N <= %d, d >= 1", kBigMaxClients);
+  *bytes = round_partial_bytes(static_cast<int>(n), d) + 256;
   return SRA_OK;
 }
 
@@ -1328,7 +1328,7 @@ extern "C" int sra_bulyan_round_f32(const float* X, int64_t n, int64_t d, int64_
   SRA_REQUIRE(mode == kBulyanMedian || mode == kBulyanTrimmed, SRA_ERR_ARG, "round mode must be median (1) or "
               "trimmedmean (2), got %d", mode);
   size_t need = 0;
-  sra_bulyan_round_workspace_bytes(n, &need);
+  sra_bulyan_round_workspace_bytes(n, d, &need);
   SRA_REQUIRE(ws_bytes >= need, SRA_ERR_WORKSPACE, "bulyan round workspace too small: need %zu bytes", need);
   return launch_bulyan_round(X, static_cast<int>(n), d, ldx, rows, nr, mode, dba != 0, agg, static_cast<float*>(ws),
                              dist, static_cast<hipStream_t>(stream));

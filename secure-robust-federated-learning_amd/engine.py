@@ -211,7 +211,7 @@ def bulyan_round(X, rows, nr, aggsubfunc, agg, dist, dba=False):
     distances over this block's columns).  No host synchronisation."""
     X, n, d, ldx = as_matrix(X)
     mode = BULYAN_MODES[aggsubfunc]
-    nb = _lib.query_bytes("sra_bulyan_round_workspace_bytes", n)
+    nb = _lib.query_bytes("sra_bulyan_round_workspace_bytes", n, d)
     ws = _workspace(nb, X.device)
     _lib.call("sra_bulyan_round_f32", X.data_ptr(), n, d, ldx, rows.data_ptr(), int(nr), mode, int(bool(dba)),
               agg.data_ptr(), dist.data_ptr(), ws.data_ptr(), nb, _stream_ptr(X.device))
