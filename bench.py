@@ -42,6 +42,8 @@ engine = shard = None   # srfl_amd modules, bound by _load_engine() once this pr
 
 def _load_engine():
     global engine, shard
+    if engine is not None:
+        return
     import srfl_loader
     srfl_loader.load()
     from srfl_amd import engine as _e, shard as _s
@@ -212,7 +214,7 @@ KERNEL_NAME = {
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
     "krum": "whole krum op (bf16x3 gram_partial_kernel dominant; per-kernel split in profiles/)",
-    "mom_krum": "whole mom_krum op (bucket means + bf16x3 Gram + scoring)",
+    "mom_krum": "whole mom_krum op (gram_bucket_kernel: bucket means fused into the bf16x3 Gram + scoring)",
     "bulyankrum": "whole bulyan op (bf16x3 Gram + theta Krum rounds + final stage)",
     "bulyanmedian": "whole bulyan op (theta fused select+distance rounds + final stage)",
     "bulyantrimmedmean": "whole bulyan op (theta fused select+distance rounds + final stage)",
@@ -253,8 +255,9 @@ def roofline_model(agg, n, d):
     if agg == "krum":
         return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d
     if agg == "mom_krum":
-        m = -(-n // 3)
-        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 2 * 4 * m * d   # buckets: read X, write + re-read means
+        # the clients read once (the bucket means are formed inside the Gram's
+        # loads, gram_bucket.hip) and the chosen bucket's mean row written
+        return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * d
     if agg == "bulyankrum":
         theta = n - 40
         return "hbm", HBM_PEAK_GBS, "GB/s", 4 * n * d + 4 * theta * d + 8 * d   # Gram, final stage, out
@@ -328,6 +331,7 @@ def secondary_roofline(agg, n, d, kern_ms):
 def filter_into(agg):
     """(X_cols, out_view) form of a spectral filter for the pipelined path: the
     block's result is written straight into its slot of the all-gather buffer."""
+    _load_engine()
     ffn = {"filterl2": engine.filter_l2, "ex_noregret": engine.ex_noregret,
            "mom_filterl2": engine.mom_filter_l2, "mom_ex_noregret": engine.mom_ex_noregret}[agg]
     kw = dict(FILTER_ARGS, check=False)
@@ -455,8 +459,7 @@ def main():
         if a.agg == "krum":
             sharded = lambda: shard.krum(ops["gram"], ops["krum_select"], X, dtot, 20)[0]
         elif a.agg == "mom_krum":
-            nb = -(-n // 3)
-            sharded = lambda: shard.krum(ops["gram"], ops["krum_select"], engine.bucket_means(X, 3, nb), dtot, 20)[0]
+            sharded = lambda: shard.mom_krum(ops, X, dtot, 20)[0]
         else:
             sharded = lambda: shard.bulyan(ops, X, dtot, 20, a.agg[len("bulyan"):])
     # N>1, coordinate-wise: block-cyclic shard (this rank's X = its blocks side

@@ -132,6 +132,24 @@ int sra_gather_rows_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const
 int sra_bucket_mean_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size, int32_t nbuckets,
                         float* out, int64_t ldo, void* stream);
 
+/* mom_krum (src/robust_estimator.py:250-256) without the bucket matrix: the
+ * Gram of the nb = ceil(n / bucket_size) bucket means is formed straight from
+ * the client rows (each read once), Krum picks over the buckets as
+ * sra_krum_select_f32 with rounds = 1 (order[0] = the bucket), and out (d
+ * floats) receives that bucket's mean, bit for bit sra_bucket_mean_f32's row.
+ * 1 <= bucket_size <= 4 and nb <= 192, else SRA_ERR_UNSUPPORTED (the caller
+ * then takes sra_bucket_mean_f32 + sra_krum_select_f32). */
+/* The centred Gram (nb x nb fp64, nb = ceil(n / bucket_size)) of the bucket
+ * means of sra_bucket_mean_f32, formed from the client rows without writing
+ * the means (mom_krum's distances; per column shard, summed by all-reduce for
+ * a sharded mom_krum).  Workspace: sra_gram_workspace_bytes(nb, d).  1 <=
+ * bucket_size <= 4, nb <= 192. */
+int sra_gram_buckets_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size, double* G,
+                         void* ws, size_t ws_bytes, void* stream);
+int sra_mom_krum_workspace_bytes(int64_t n, int64_t d, int32_t bucket_size, size_t* bytes);
+int sra_mom_krum_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t bucket_size,
+                     int32_t* order, float* out, void* ws, size_t ws_bytes, void* stream);
+
 
 /* ------------------------------------------------------------------------ */
 /* Bulyan (k4)                                                               */

@@ -531,6 +531,35 @@ static int launch_gram_nb(const float* X, int n, int64_t d, int64_t ldx, double*
   return launch_gram_nbw<NB, 8>(X, n, d, ldx, G, slab, s, pr);
 }
 
+// Gram of the bucket means (gram_bucket.hip) + the fixed-order fp64 reduction
+template <int NB>
+static int gram_reduce_slab(const float* slab, int64_t nslab, int n, double* G, hipStream_t s) {
+  using C = GramCfg<NB>;
+  double* partial = reinterpret_cast<double*>(const_cast<float*>(slab) + nslab * C::T * 1024);
+  hipLaunchKernelGGL((gram_reduce1_kernel<NB>), dim3(cdiv(C::T * 1024, 256), kRedGroups), dim3(256), 0, s, slab, nslab,
+                     partial);
+  const int rc = launch_status("gram_reduce1_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL((gram_reduce2_kernel<NB>), dim3(cdiv(C::T * 1024, 256)), dim3(256), 0, s, partial, n, G);
+  return launch_status("gram_reduce2_kernel");
+}
+
+int launch_gram_buckets(const float* X, int n, int bs, int64_t d, int64_t ldx, double* G, float* slab,
+                        hipStream_t s) {
+  const int nb = static_cast<int>(cdiv(n, bs));
+  const int nwg = gram_num_wg(d);
+  const int rc = launch_gram_bucket_partial(X, n, nb, bs, d, ldx, slab, nwg, s);
+  if (rc) return rc;
+  switch (cdiv(nb, 32)) {
+    case 1: return gram_reduce_slab<1>(slab, nwg, nb, G, s);
+    case 2: return gram_reduce_slab<2>(slab, nwg, nb, G, s);
+    case 3: return gram_reduce_slab<3>(slab, nwg, nb, G, s);
+    case 4: return gram_reduce_slab<4>(slab, nwg, nb, G, s);
+    case 5: return gram_reduce_slab<5>(slab, nwg, nb, G, s);
+    default: return gram_reduce_slab<6>(slab, nwg, nb, G, s);
+  }
+}
+
 constexpr int kGramMaxClients = 512;
 constexpr int kGramPairRows = 128;
 
@@ -605,4 +634,18 @@ extern "C" int sra_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, d
   SRA_REQUIRE(X != nullptr && G != nullptr, SRA_ERR_ARG, "null pointer");
   SRA_REQUIRE(d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad d/ldx (%lld/%lld)", (long long)d, (long long)ldx);
   return sra::launch_gram(X, static_cast<int>(n), d, ldx, G, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_gram_buckets_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size, double* G,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && G != nullptr && ws != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= (int64_t(1) << 30) && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape");
+  SRA_REQUIRE(bucket_size >= 1 && bucket_size <= 4 && sra::cdiv(n, bucket_size) <= 32 * sra::kBucketGramMaxNB,
+              SRA_ERR_UNSUPPORTED, "bucket Gram: 1 <= bucket size <= 4 and at most %d buckets",
+              32 * sra::kBucketGramMaxNB);
+  const int nb = static_cast<int>(sra::cdiv(n, bucket_size));
+  SRA_REQUIRE(ws_bytes >= sra::gram_workspace_bytes(nb, d), SRA_ERR_WORKSPACE,
+              "bucket Gram workspace too small: need %zu bytes", sra::gram_workspace_bytes(nb, d));
+  return sra::launch_gram_buckets(X, static_cast<int>(n), bucket_size, d, ldx, G, static_cast<float*>(ws),
+                                  static_cast<hipStream_t>(stream));
 }

@@ -92,4 +92,10 @@ __host__ __device__ constexpr bool gram_pipe_offsets_fit(int64_t ldx) {
 }
 int launch_gram_pipe(const float* X, int n, int64_t d, int64_t ldx, float* slab, int nwg, hipStream_t s);
 
+// gram_bucket.hip: the Gram of the means of consecutive client buckets of size
+// bs (mom_krum), the bucket matrix never written; nb = ceil(n / bs) buckets.
+constexpr int kBucketGramMaxNB = 6;   // at most 192 buckets
+int launch_gram_bucket_partial(const float* X, int n, int nb, int bs, int64_t d, int64_t ldx, float* slab, int nwg,
+                               hipStream_t s);
+
 }  // namespace sra

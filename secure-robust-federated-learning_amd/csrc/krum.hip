@@ -15,7 +15,7 @@
 // a theta-round Bulyan-Krum costs theta * N^2 instead of theta * N^2 log N.
 // Everything runs in one workgroup: N-space work is microseconds and needs no
 // host synchronisation between rounds.
-#include "sra_common.hpp"
+#include "gram_common.hpp"
 
 namespace sra {
 
@@ -63,8 +63,21 @@ __global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __r
 // any term is -- so no special value ever goes through the float atomic.
 constexpr int kDirTile = 32;
 constexpr int kDirK = 64;
+// element k of row i of the matrix Krum scores: X itself (bs == 1), or the
+// mean of the bucket of clients [i*bs, min((i+1)*bs, nx)) with bucket.hip's
+// expression (mom_krum's fused route, which never writes the bucket means)
+__device__ __forceinline__ float row_value(const float* __restrict__ X, int64_t ldx, int nx, int bs, int i,
+                                           int64_t k) {
+  if (bs == 1) return X[static_cast<int64_t>(i) * ldx + k];
+  const int lo = i * bs;
+  const int hi = lo + bs < nx ? lo + bs : nx;
+  float acc = 0.f;
+  for (int q = lo; q < hi; ++q) acc += X[static_cast<int64_t>(q) * ldx + k];
+  return acc / static_cast<float>(hi - lo);
+}
+
 __global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
-                                                          const int* __restrict__ nonfinite,
+                                                          int nx, int bs, const int* __restrict__ nonfinite,
                                                           double* __restrict__ acc, int* __restrict__ cls,
                                                           int nslices) {
   if (*nonfinite == 0) return;
@@ -86,8 +99,8 @@ __global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restric
       const int r = e / kDirK, c = e % kDirK;
       const int64_t k = kb + c;
       const int ra = I * kDirTile + r, rb = J * kDirTile + r;
-      ta[r][c] = (ra < n && k < k1) ? X[static_cast<int64_t>(ra) * ldx + k] : 0.f;
-      tb[r][c] = (rb < n && k < k1) ? X[static_cast<int64_t>(rb) * ldx + k] : 0.f;
+      ta[r][c] = (ra < n && k < k1) ? row_value(X, ldx, nx, bs, ra, k) : 0.f;
+      tb[r][c] = (rb < n && k < k1) ? row_value(X, ldx, nx, bs, rb, k) : 0.f;
     }
     __syncthreads();
 #pragma unroll 4
@@ -394,7 +407,7 @@ size_t krum_workspace_bytes(int n, int64_t d) {
 // its flag and n x n fp64 accumulator
 static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* order, float* scores0, char* ws,
                               const float* X, int64_t d, int64_t ldx, int* nonfinite, double* acc, int* cls,
-                              hipStream_t s) {
+                              hipStream_t s, int nx = 0, int bs = 1) {
   const size_t nn = static_cast<size_t>(n) * n;
   float* D = reinterpret_cast<float*>(ws);
   float* S = D + nn;
@@ -409,7 +422,7 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
     const int64_t kb = cdiv(d, kDirK);
     const int slices = static_cast<int>(kb < 256 ? kb : 256);
     hipLaunchKernelGGL(krum_direct_kernel, dim3(slices, nt * (nt + 1) / 2), dim3(256), 0, s, X, n, d, ldx,
-                       nonfinite, acc, cls, slices);
+                       bs == 1 ? n : nx, bs, nonfinite, acc, cls, slices);
     rc = launch_status("krum_direct_kernel");
     if (rc) return rc;
   }
@@ -476,9 +489,66 @@ int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds
   return launch_krum_rounds(G, n, f, rounds, order, scores0, rest, X, d, ldx, nonfinite, acc, cls, s);
 }
 
+// mom_krum (src/robust_estimator.py:250-256) without the bucket matrix: the
+// Gram of the bucket means straight from the clients (gram_bucket.hip), Krum
+// over the nb = ceil(n / bs) buckets (the exact route, when flagged, forms the
+// means on the fly), then the chosen bucket's mean row.
+int launch_gram_buckets(const float* X, int n, int bs, int64_t d, int64_t ldx, double* G, float* slab,
+                        hipStream_t s);
+
+__global__ void __launch_bounds__(256) bucket_row_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
+                                                         int bs, int nb, const int* __restrict__ order,
+                                                         float* __restrict__ out) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= d) return;
+  out[k] = row_value(X, ldx, n, bs, checked_row(order[0], nb), k);
+}
+
+int launch_mom_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int bs, int* order, float* out, void* ws,
+                    size_t ws_bytes, hipStream_t s) {
+  SRA_REQUIRE(n >= 1 && bs >= 1 && bs <= 4, SRA_ERR_UNSUPPORTED, "fused mom_krum: 1 <= bucket size <= 4 (got %d)",
+              bs);
+  const int nb = static_cast<int>(cdiv(n, bs));
+  SRA_REQUIRE(nb <= 32 * kBucketGramMaxNB, SRA_ERR_UNSUPPORTED, "fused mom_krum: at most %d buckets (got %d)",
+              32 * kBucketGramMaxNB, nb);
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= krum_workspace_bytes(nb, d), SRA_ERR_WORKSPACE,
+              "mom_krum workspace too small: need %zu bytes", krum_workspace_bytes(nb, d));
+  const size_t nn = static_cast<size_t>(nb) * nb;
+  char* base = static_cast<char*>(ws);
+  int* nonfinite = reinterpret_cast<int*>(base);
+  double* G = reinterpret_cast<double*>(base + 256);
+  double* acc = G + nn;
+  int* cls = reinterpret_cast<int*>(acc + nn);
+  char* rest = reinterpret_cast<char*>(cls + nn);
+  float* slab = reinterpret_cast<float*>(rest + nn * 4 * 3);
+  int rc = launch_gram_buckets(X, n, bs, d, ldx, G, slab, s);
+  if (rc) return rc;
+  rc = launch_krum_rounds(G, nb, f, 1, order, nullptr, rest, X, d, ldx, nonfinite, acc, cls, s, n, bs);
+  if (rc) return rc;
+  hipLaunchKernelGGL(bucket_row_kernel, dim3(cdiv(d, 256)), dim3(256), 0, s, X, n, d, ldx, bs, nb, order, out);
+  return launch_status("bucket_row_kernel");
+}
+
 }  // namespace sra
 
 using namespace sra;
+
+extern "C" int sra_mom_krum_workspace_bytes(int64_t n, int64_t d, int32_t bucket_size, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && d >= 1 && bucket_size >= 1 && bucket_size <= 4 &&
+                  cdiv(n, bucket_size) <= 32 * kBucketGramMaxNB, SRA_ERR_UNSUPPORTED,
+              "fused mom_krum: 1 <= bucket size <= 4, at most %d buckets", 32 * kBucketGramMaxNB);
+  *bytes = krum_workspace_bytes(static_cast<int>(cdiv(n, bucket_size)), d);
+  return SRA_OK;
+}
+
+extern "C" int sra_mom_krum_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t bucket_size,
+                                int32_t* order, float* out, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && order != nullptr && out != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= (int64_t(1) << 30) && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape");
+  return launch_mom_krum(X, static_cast<int>(n), d, ldx, f, bucket_size, order, out, ws, ws_bytes,
+                         static_cast<hipStream_t>(stream));
+}
 
 extern "C" int sra_krum_workspace_bytes(int64_t n, int64_t d, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");

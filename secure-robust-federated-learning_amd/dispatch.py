@@ -169,13 +169,9 @@ def _device_round(agg, st, args, state, local_grads, choices):
         orders = [engine.krum_select(st.cols(l), f, 1, scores=False)[0] for l in range(st.nlayers)]
         return None, torch.cat(orders)
     if agg == "clustering":
-        n = int(X.shape[0])
-        B = engine.bucket_means(X, 3, -(-n // 3))
         out = torch.empty(seg[-1], dtype=torch.float32, device=X.device)
         for l in range(st.nlayers):
-            lo, hi = seg[l], seg[l + 1]
-            order, _ = engine.krum_select(B[:, lo:hi], f, 1, scores=False)
-            engine.gather_rows(B[:, lo:hi], order, out=out[lo:hi].view(1, hi - lo))
+            out[seg[l]:seg[l + 1]] = engine.mom_krum(st.cols(l), f)[0]
         return out, None
     if agg in _BULYAN:
         out = torch.empty(seg[-1], dtype=torch.float64, device=X.device)

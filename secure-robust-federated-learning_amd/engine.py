@@ -164,10 +164,38 @@ def bucket_means(X, bucket_size, nbuckets, out=None):
     return out
 
 
-def mom_krum(X, f, bucket_size=3):
-    """robust_estimator.mom_krum on device: Krum over ceil(N/3) bucket means."""
-    n = int(X.shape[0])
+MOM_KRUM_FUSED_MAX_BUCKETS = 192
+
+
+def gram_buckets(X, bucket_size=3):
+    """Centred Gram (B x B float64) of the means of consecutive buckets of
+    clients, B = ceil(N / bucket_size) <= 192, without writing the means."""
+    X, n, d, ldx = as_matrix(X)
     nb = -(-n // bucket_size)
+    G = torch.empty((nb, nb), dtype=torch.float64, device=X.device)
+    nbytes = _lib.query_bytes("sra_gram_workspace_bytes", nb, d)
+    ws = _workspace(nbytes, X.device)
+    _lib.call("sra_gram_buckets_f32", X.data_ptr(), n, d, ldx, int(bucket_size), G.data_ptr(), ws.data_ptr(), nbytes,
+              _stream_ptr(X.device))
+    return G
+
+
+def mom_krum(X, f, bucket_size=3, fused=True):
+    """robust_estimator.mom_krum on device: Krum over ceil(N/3) bucket means.
+    Returns (the chosen bucket's mean row (d,), order int32 (1,) = its bucket).
+    Up to 192 buckets of at most 4 clients the bucket means are never written
+    (sra_mom_krum_f32); otherwise, or with fused=False, they are materialised
+    (sra_bucket_mean_f32) and scored by krum()."""
+    X, n, d, ldx = as_matrix(X)
+    nb = -(-n // bucket_size)
+    if fused and 1 <= bucket_size <= 4 and nb <= MOM_KRUM_FUSED_MAX_BUCKETS:
+        out = torch.empty(d, dtype=torch.float32, device=X.device)
+        order = torch.empty(1, dtype=torch.int32, device=X.device)
+        nbytes = _lib.query_bytes("sra_mom_krum_workspace_bytes", n, d, int(bucket_size))
+        ws = _workspace(nbytes, X.device)
+        _lib.call("sra_mom_krum_f32", X.data_ptr(), n, d, ldx, int(f), int(bucket_size), order.data_ptr(),
+                  out.data_ptr(), ws.data_ptr(), nbytes, _stream_ptr(X.device))
+        return out, order
     B = bucket_means(X, bucket_size, nb)
     row, order = krum(B, f)
     return row, order

@@ -92,6 +92,25 @@ def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
     return row, idx
 
 
+def mom_krum(ops, X_shard, d, f, bucket_size=3, group=None, align=1):
+    """mom_krum (robust_estimator.py:250-256) over a column-sharded layer.
+
+    The centred Gram of the bucket means decomposes over columns like Krum's:
+    each rank forms its partial from its own columns without writing the means
+    (``ops["gram_buckets"]``), one all-reduce of B x B doubles sums them, every
+    rank picks the same bucket (``ops["krum_select"]``), and the bucket's mean
+    over each rank's columns (``ops["bucket_mean"]``, np.mean order) is
+    all-gathered.  Returns (full mean row of the chosen bucket, bucket index)."""
+    n = int(X_shard.shape[0])
+    G = ops["gram_buckets"](X_shard, bucket_size).to(torch.float64).contiguous()
+    if dist.is_initialized():
+        dist.all_reduce(G, op=dist.ReduceOp.SUM, group=group)
+    idx = int(ops["krum_select"](G, f))
+    lo = idx * bucket_size
+    part = ops["bucket_mean"](X_shard[lo:min(lo + bucket_size, n)])
+    return gather_columns(part, d, align, group), idx
+
+
 def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
     """Bulyan (robust_estimator.py:277-332) over a column-sharded layer.
 
@@ -246,6 +265,8 @@ def engine_ops():
         "median": lambda X: engine.median(X),
         "trimmedmean": lambda X: engine.trimmed_mean(X, 0.1),
         "gram": gram_fn,
+        "gram_buckets": lambda X, bs: engine.gram_buckets(X, bs),
+        "bucket_mean": lambda R: engine.bucket_means(R, int(R.shape[0]), 1)[0],
         "krum_select": select_fn,
         # (X_cols, out_view) forms for pipelined_coordinatewise
         "average_into": lambda X, o: engine.average(X, out=o),

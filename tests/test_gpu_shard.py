@@ -59,6 +59,17 @@ def test_sharded_krum_bit_exact(nccl_group):
     assert torch.equal(row, want_row)
 
 
+def test_sharded_mom_krum_bit_exact(nccl_group):
+    """bench.py's N > 1 mom_krum path: the bucket Gram all-reduced through RCCL,
+    the chosen bucket's mean all-gathered; equal to the unsharded fused op."""
+    x = make_rows(512, 20_000, seed=34, byz=60)
+    X = torch.from_numpy(x).cuda()
+    row, idx = shard.mom_krum(shard.engine_ops(), X, 20_000, 20)
+    want_row, order = engine.mom_krum(X, 20)
+    assert idx == int(order.cpu()[0])
+    assert torch.equal(row, want_row)
+
+
 @pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
 def test_sharded_bulyan_bit_exact(nccl_group, mode):
     x = make_rows(64, 12_000, seed=33, byz=10)

@@ -133,6 +133,22 @@ def _worker(rank, world, port, results):
         row, idx = shard.krum(lambda X: torch.from_numpy(_centred_gram(X.numpy())), select, Xk, 777, 6)
         out["krum_row"] = row.numpy()
         out["krum_idx"] = idx
+        # mom_krum: all-reduced partial Gram of the bucket means, the chosen
+        # bucket's mean formed per shard and all-gathered
+        xm = make_rows(31, 777, seed=15, byz=9)
+        Xm = torch.from_numpy(np.ascontiguousarray(xm[:, lo:hi]))
+
+        def gram_buckets(X, bs):
+            x = X.numpy()
+            nb = -(-x.shape[0] // bs)
+            return torch.from_numpy(_centred_gram(np.array(orc.bucket_means(list(x), bs, nb))))
+
+        mops = {"gram_buckets": gram_buckets, "krum_select": select,
+                "bucket_mean": lambda R: torch.from_numpy(np.asarray(orc.bucket_means(list(R.numpy()),
+                                                                                     R.shape[0], 1)[0]))}
+        row, idx = shard.mom_krum(mops, Xm, 777, 2)
+        out["mom_krum_row"] = row.numpy()
+        out["mom_krum_idx"] = idx
         # block-cyclic shard + pipelined in-place all-gather, ragged last round
         for block in (64, 96, 1001):
             cols = shard.cyclic_blocks(d, world, rank, block)
@@ -292,6 +308,18 @@ def test_sharded_krum_equals_unsharded(two_rank_results):
     for r in (0, 1):
         assert two_rank_results[r]["krum_idx"] == idx
         np.testing.assert_array_equal(two_rank_results[r]["krum_row"], row)
+
+
+def test_sharded_mom_krum_equals_unsharded(two_rank_results):
+    _setup_paths()
+    from oracle import robust_np as orc
+    from synth import make_rows
+    xm = make_rows(31, 777, seed=15, byz=9)
+    want = orc.mom_krum(list(xm), 2)
+    bm = orc.bucket_means(list(xm), 3, 11)
+    for r in (0, 1):
+        np.testing.assert_array_equal(two_rank_results[r]["mom_krum_row"], want)
+        np.testing.assert_array_equal(bm[two_rank_results[r]["mom_krum_idx"]], want)
 
 
 @pytest.mark.parametrize("mode", ["krum", "median", "trimmedmean"])
