@@ -106,7 +106,10 @@ int sra_krum_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
  *  picks the first minimum and removes it; order[t] = its client index.
  *  rounds = 1 is robust_estimator.krum (src/robust_estimator.py:246-249);
  *  rounds = theta is the selection of bulyan(aggsubfunc='krum') (:286-296).
- *  scores (optional, n floats) receive round 0's scores = krum_'s metric. */
+ *  scores (optional, n floats) receive round 0's scores = krum_'s metric.
+ *  Distances: from the centred Gram for d > 1024; for d <= 1024, or data with
+ *  a NaN / inf, each pair's fp32 difference squared and summed in fp64 (the
+ *  reference's np.linalg.norm of the difference, :242). */
 int sra_krum_select_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t rounds,
                         int32_t* order, float* scores, void* ws, size_t ws_bytes, void* stream);
 

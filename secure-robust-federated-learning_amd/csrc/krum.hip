@@ -63,6 +63,7 @@ __global__ void krum_dist_kernel(const double* __restrict__ G, int n, float* __r
 // any term is -- so no special value ever goes through the float atomic.
 constexpr int kDirTile = 32;
 constexpr int kDirK = 64;
+constexpr int64_t kExactMaxD = 1024;
 // element k of row i of the matrix Krum scores: X itself (bs == 1), or the
 // mean of the bucket of clients [i*bs, min((i+1)*bs, nx)) with bucket.hip's
 // expression (mom_krum's fused route, which never writes the bucket means)
@@ -412,7 +413,12 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
   float* D = reinterpret_cast<float*>(ws);
   float* S = D + nn;
   int* J = reinterpret_cast<int*>(S + nn);
-  if (X != nullptr) SRA_HIP(hipMemsetAsync(nonfinite, 0, sizeof(int), s));
+  // narrow layers (d <= kExactMaxD) always take the exact route: with few
+  // coordinates the nearest pairs sit far below the rows' norms, where the
+  // Gram's G_ii + G_jj - 2 G_ij loses the bits the reference's fp32 norm of
+  // the difference keeps (one slice per tile pair: no atomics, deterministic)
+  const bool narrow = X != nullptr && d <= kExactMaxD;
+  if (X != nullptr) SRA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(nonfinite), narrow ? 1 : 0, 1, s));
   hipLaunchKernelGGL(krum_dist_kernel, dim3(cdiv(n * n, 256)), dim3(256), 0, s, G, n, D, X ? nonfinite : nullptr,
                      X ? acc : nullptr, X ? cls : nullptr);
   int rc = launch_status("krum_dist_kernel");
@@ -420,7 +426,7 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
   if (X != nullptr && n > 1) {
     const int nt = static_cast<int>(cdiv(n, kDirTile));
     const int64_t kb = cdiv(d, kDirK);
-    const int slices = static_cast<int>(kb < 256 ? kb : 256);
+    const int slices = narrow ? 1 : static_cast<int>(kb < 256 ? kb : 256);
     hipLaunchKernelGGL(krum_direct_kernel, dim3(slices, nt * (nt + 1) / 2), dim3(256), 0, s, X, n, d, ldx,
                        bs == 1 ? n : nx, bs, nonfinite, acc, cls, slices);
     rc = launch_status("krum_direct_kernel");
