@@ -1023,13 +1023,6 @@ __global__ void __launch_bounds__(64) bulyan_coord_f64_kernel(const double* __re
 // host orchestration
 // ---------------------------------------------------------------------------
 
-// bulyan_rank.hip: the rounds on persistent per-coordinate ranks (N <= 128)
-constexpr int kRankMaxClients = 128;
-int launch_rank_init(const float* X, int64_t ldx, int n, int64_t d, uint8_t* ranks, hipStream_t s);
-int launch_rank_round(const float* X, int64_t ldx, const int* rows, int nrows_x, int n, int64_t d, bool median,
-                      int lo, int hi, uint8_t* ranks, const int* picked, float* out, float* bpart, int nb, int tpb,
-                      hipStream_t s);
-
 // workspace: [0, 256) nonfinite-column count | order, row lists, status |
 // krum workspace or (S, partial sums) | the nonfinite-column list (int64 x d)
 static size_t bulyan_body_bytes(int n, int64_t d, int mode, int f) {
@@ -1040,7 +1033,6 @@ static size_t bulyan_body_bytes(int n, int64_t d, int mode, int f) {
   } else {
     b += sizeof(float) * static_cast<size_t>(theta > 0 ? theta : 0) * static_cast<size_t>(d) + 256;
     b += round_partial_bytes(n, d) + sizeof(double) * static_cast<size_t>(n) + 512;
-    if (n <= kRankMaxClients) b += static_cast<size_t>(n) * static_cast<size_t>(d) + 256;   // uint8 ranks
   }
   return (b + 255) / 256 * 256;
 }
@@ -1144,9 +1136,8 @@ static int launch_round_big(const float* X, int64_t ldx, const int* rows, int nr
   return launch_status("dist_rows_kernel");
 }
 
-// the aggregate of a round over nr clients: sel_mode 0 = numpy's median, 1 =
-// the sequential fp32 mean of the sorted window [lo, hi)
-static void round_window(int nr, int mode, bool dba, int* lo_out, int* hi_out, int* sel_out) {
+static int launch_bulyan_round(const float* X, int nrows_x, int64_t d, int64_t ldx, const int* rows, int nr, int mode,
+                               bool dba, float* agg, float* bpart, double* dist, hipStream_t s) {
   int lo, hi, sel_mode;
   if (mode == kBulyanMedian && dba) {
     lo = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
@@ -1162,15 +1153,6 @@ static void round_window(int nr, int mode, bool dba, int* lo_out, int* hi_out, i
     hi = nr - b > b ? nr - b : b;
     sel_mode = 1;
   }
-  *lo_out = lo;
-  *hi_out = hi;
-  *sel_out = sel_mode;
-}
-
-static int launch_bulyan_round(const float* X, int nrows_x, int64_t d, int64_t ldx, const int* rows, int nr, int mode,
-                               bool dba, float* agg, float* bpart, double* dist, hipStream_t s) {
-  int lo, hi, sel_mode;
-  round_window(nr, mode, dba, &lo, &hi, &sel_mode);
   int rc;
   if (nr > 128)
     rc = launch_round_big(X, ldx, rows, nrows_x, nr, d, sel_mode == 0, lo, hi, agg, bpart, s);
@@ -1233,34 +1215,6 @@ int launch_bulyan(const float* X, int n, int64_t d, int64_t ldx, int f, int mode
       (reinterpret_cast<uintptr_t>(bpart) + round_partial_bytes(n, d) + 255) & ~static_cast<uintptr_t>(255));
   int* cur = rows_a;
   int* nxt = rows_b;
-  if (n <= kRankMaxClients) {
-    // the rounds on persistent ranks: one sort per column, then per round one
-    // read of the remaining rows (bulyan_rank.hip)
-    uint8_t* ranks = reinterpret_cast<uint8_t*>(
-        (reinterpret_cast<uintptr_t>(dist) + sizeof(double) * static_cast<size_t>(n) + 255) & ~static_cast<uintptr_t>(255));
-    int* picked = rows_b + n + 1;
-    const int64_t tpb = round_tiles_per_block(d);
-    const int nbk = static_cast<int>(round_blocks(d));
-    rc = launch_rank_init(X, ldx, n, d, ranks, s);
-    if (rc) return rc;
-    for (int t = 0; t < theta; ++t) {
-      const int nr = n - t;
-      int lo, hi, sel_mode;
-      round_window(nr, mode, dba, &lo, &hi, &sel_mode);
-      float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);
-      rc = launch_rank_round(X, ldx, cur, n, nr, d, sel_mode == 0, lo, hi, ranks, t == 0 ? nullptr : picked, agg,
-                             bpart, nbk, static_cast<int>(tpb), s);
-      if (rc) return rc;
-      hipLaunchKernelGGL(bulyan_dist_reduce_kernel, dim3(nr), dim3(256), 0, s, bpart, nbk, dist);
-      hipLaunchKernelGGL(bulyan_pick_kernel, dim3(1), dim3(256), 0, s, dist, cur, nr, nxt, status, picked);
-      rc = launch_status("bulyan_pick_kernel");
-      if (rc) return rc;
-      int* tmp = cur;
-      cur = nxt;
-      nxt = tmp;
-    }
-    return launch_final(S, d, order, theta, theta, beta, d, out, nf_count, nf_list, s);
-  }
   for (int t = 0; t < theta; ++t) {
     const int nr = n - t;
     float* agg = S + static_cast<size_t>(t) * static_cast<size_t>(d);

@@ -1,9 +1,9 @@
-"""Bulyan's median / trimmed-mean rounds on persistent ranks (csrc/bulyan_rank.hip,
-taken by engine.bulyan for N <= 128) against the per-round sorting kernels
-(select_dist_rows_kernel, reached through shard.bulyan's per-round
-engine.bulyan_round / bulyan_pick with no process group): the two must give
-the same selection and the same float64 result bit for bit -- ragged tiles,
-tied values, signed zeros, infinities, every P bucket of the row count."""
+"""Bulyan's median / trimmed-mean selection: engine.bulyan (all rounds in one
+sra_bulyan_f32 call) against the per-round C ABI a sharded layer uses
+(sra_bulyan_round_f32 + sra_bulyan_pick, reached through shard.bulyan with no
+process group): the same selection and the same float64 result bit for bit --
+ragged tiles, tied values, signed zeros, infinities, every P bucket of the row
+count (src/robust_estimator.py:297-332)."""
 from __future__ import annotations
 
 import numpy as np
