@@ -50,3 +50,4 @@ for x in list(csv.DictReader(open('$OUT/prof_$name/run_kernel_stats.csv')))[:8]:
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
+exit 0

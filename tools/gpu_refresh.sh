@@ -10,6 +10,7 @@ export TMPDIR=/tmp
 W="default|--agg trimmedmean --steps 20
 median|--agg median --steps 20
 average|--agg average --steps 20
+c2_trimmedmean_d1e6|--agg trimmedmean --d 1e6 --steps 50
 trimmedmean_n100|--agg trimmedmean --clients 100 --steps 20
 median_n100|--agg median --clients 100 --steps 20
 trimmedmean_n512|--agg trimmedmean --clients 512 --d 1.25e7
