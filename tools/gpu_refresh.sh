@@ -35,5 +35,6 @@ while IFS='|' read -r name args; do
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run \
     -- python3 "$R/bench.py" --warmup 1 --no-cpu --no-host $args > "$OUT/prof_$name.log" 2>&1) \
     || { echo "prof $name failed rc=$?"; exit 1; }
+  rm -f "$OUT/prof_$name"/run_kernel_trace.csv "$OUT/prof_$name"/run_agent_info.csv   # keep the stats (<64 MiB back)
   echo "prof $name ok"
 done <<< "$W"

@@ -28,7 +28,7 @@ DOMINANT = {"trimmedmean": "select_plain_kernel", "median": "select_reg_kernel",
 # (launches under 10 % of the largest anchor's fetch are bench.py's small
 # side calls, e.g. the solver-flop probe on 1000 columns, and are not counted)
 WHOLE_OP = {"filterl2": "chunk_gram", "ex_noregret": "chunk_gram", "mom_filterl2": "chunk_gram",
-            "mom_ex_noregret": "chunk_gram", "bulyankrum": "gram_partial_kernel", "mom_krum": "gram_partial_kernel",
+            "mom_ex_noregret": "chunk_gram", "bulyankrum": "gram_partial_kernel", "mom_krum": "gram_bucket_kernel",
             "bulyanmedian": "bulyan_final", "bulyantrimmedmean": "bulyan_final"}
 
 
