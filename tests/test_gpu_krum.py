@@ -92,7 +92,7 @@ def test_identical_rows_zero_distance_and_unaligned():
 
 
 @pytest.mark.parametrize("n,f", [(128, 20), (100, 20), (64, 10), (20, 25), (129, 20), (200, 20), (256, 40),
-                                 (300, 20), (512, 50)])
+                                 (300, 20), (512, 50), (512, 10), (512, 3)])   # m = 500, 507: three split levels
 def test_krum_index_against_oracle(n, f):
     d = 20_000 if n <= 256 else 4_000
     x = make_rows(n, d, seed=300 + n, byz=min(f, n // 3))
