@@ -1665,6 +1665,14 @@ constexpr size_t kLanczosLds =
     sizeof(double) * (136 + 2 * 136 + 32 + kTrw + 2 * MMAX + kCheckScr + 64 + 4 * FNP + 240) +
     sizeof(int) * (3 * FNP + 16);
 static_assert(3 * kLanczosLds <= 163840, "three solver workgroups must fit one CU's LDS");
+// The first kLdsBasis Lanczos vectors stay in LDS (the registers cap the solver
+// at two workgroups per CU, which leaves ~58 KiB of LDS each); only steps past
+// them go to the per-workgroup global scratch.  Round 3's whole-op PMC had the
+// scratch basis at 109 GB read + 33 GB written per C4 call: 512 workgroups x
+// ~70 vectors of 1 KiB do not stay in the L2.
+constexpr int kLdsBasis = 56;
+constexpr size_t kLanczosLdsTotal = kLanczosLds + sizeof(double) * kLdsBasis * FNP;
+static_assert(2 * kLanczosLdsTotal <= 163840, "two solver workgroups with their LDS basis must fit one CU");
 
 __device__ __forceinline__ double swap_halves(double v) {   // the value of lane l ^ 32
   const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
@@ -1697,6 +1705,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
   double* vscr = cvec + FNP;                        // [3][FNP] projection scratch
   double* clog = vscr + 3 * FNP;                    // [60][4] DBG: check log of the current iteration
   int* ibuf = reinterpret_cast<int*>(clog + 240);   // [3][FNP] int scratch + [16] argmax slots
+  double* lbas = reinterpret_cast<double*>(smem + kLanczosLds);   // [kLdsBasis][FNP] first basis vectors
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1706,6 +1715,10 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
   const bool own = half == 0;
   const int n = A.n;
   double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * MMAX * FNP;
+  // basis entry qq of this row: LDS for the first kLdsBasis vectors, else the scratch
+  auto vload = [&](int qq) __attribute__((always_inline)) -> double {
+    return qq < kLdsBasis ? lbas[qq * FNP + row] : Vb[qq * FNP + row];
+  };
 
   int rslot = 0;
   auto reduce2 = [&](double v0, double v1, double (&o)[4], int nv) __attribute__((always_inline)) {
@@ -1954,7 +1967,10 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
           const double y = gmv();
           const double ib = 1.0 / bet;
           const double q = rt * ib;
-          if (own) Vb[j * FNP + row] = q;
+          if (own) {
+            if (j < kLdsBasis) lbas[j * FNP + row] = q;
+            else Vb[j * FNP + row] = q;
+          }
           const double mq = y * ib;
           reduce2(own ? q * mq : 0.0, 0.0, o, 1);
           double aj = o[0];
@@ -1971,7 +1987,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
             for (int pass = 0; pass < 2; ++pass) {
               const int nh = pass == 0 ? j + 2 : j + 1;
               for (int qq = 0; qq < nh; ++qq) {
-                double v = own ? (qq <= j ? Vb[qq * FNP + row] * r : r * r) : 0.0;
+                double v = own ? (qq <= j ? vload(qq) * r : r * r) : 0.0;
                 v = wave_sum(v);
                 if (lane == 0) hs[wave * HS + qq] = v;
               }
@@ -1981,7 +1997,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
               double upd = 0.0, hn2 = 0.0;
               for (int qq = 0; qq <= j; ++qq) {
                 const double hv = hb[qq];
-                upd = fma(hv, Vb[qq * FNP + row], upd);
+                upd = fma(hv, vload(qq), upd);
                 hn2 = fma(hv, hv, hn2);
               }
               r -= upd;
@@ -2014,10 +2030,10 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
         double u0 = 0.0, u1 = 0.0;
         int qq = 0;
         for (; qq + 1 < m_conv; qq += 2) {
-          u0 = fma(zb[qq], Vb[qq * FNP + row], u0);
-          u1 = fma(zb[qq + 1], Vb[(qq + 1) * FNP + row], u1);
+          u0 = fma(zb[qq], vload(qq), u0);
+          u1 = fma(zb[qq + 1], vload(qq + 1), u1);
         }
-        if (qq < m_conv) u0 = fma(zb[qq], Vb[qq * FNP + row], u0);
+        if (qq < m_conv) u0 = fma(zb[qq], vload(qq), u0);
         ui = swi > 0.0 ? u0 + u1 : 0.0;
       }
       u_prev = ui;
@@ -2798,7 +2814,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
   const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
                            : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
-  SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLds)));
+  SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLdsTotal)));
   // ex_noregret stays on the re-orthogonalising kernel: on the plain solver
   // (217 vs 327 ms at C4) every traced decision agreed, but the C4 fixture
   // chunk 1 landed 2.9e-3 of max from the reference (bound 2e-5) and two DBA
@@ -2834,8 +2850,8 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("list_all_kernel");
       if (rc) return rc;
     } else {
-      if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<0, true>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
-      else hipLaunchKernelGGL((lanczos_solve_kernel<0, false>), dim3(lgrid), dim3(256), kLanczosLds, s, sa);
+      if (dbg) hipLaunchKernelGGL((lanczos_solve_kernel<0, true>), dim3(lgrid), dim3(256), kLanczosLdsTotal, s, sa);
+      else hipLaunchKernelGGL((lanczos_solve_kernel<0, false>), dim3(lgrid), dim3(256), kLanczosLdsTotal, s, sa);
       rc = launch_status("lanczos_solve_kernel");
       if (rc) return rc;
     }
