@@ -116,11 +116,15 @@ def _fullsize(X, mode, nsample=48, seed=0):
             np.testing.assert_array_equal(got[1 + n:], a[1 + n:], err_msg="chunk %d: kept set" % c)
     assert np.isfinite(out.cpu().numpy()).all()
     # the agreed prefixes must cover most of the run (the early iterations
-    # remove the far-out Byzantine clients; the near ties come late)
+    # remove the far-out Byzantine clients; the near ties come late).  The
+    # coverage is fixed by the data, not the device (where the oracle's own
+    # independent evaluations disagree the reference's decision is rounding):
+    # 0.884 / 1.0 / 0.921 of the decisions for the three workloads' seeds
+    # (profiles/r04_filter_trace_fullsize.txt)
     total = sum(int(a[0]) for a, _, _ in refs)
     covered = sum(ag for _, ag, _ in refs)
     print("decisions compared: %d of %d (%d chunks fully agreed)" % (covered, total, agreed))
-    assert covered >= 0.6 * total
+    assert covered >= 0.85 * total
     return agreed, len(chunks)
 
 
