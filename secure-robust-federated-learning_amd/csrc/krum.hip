@@ -284,20 +284,42 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
     const int m = slice_count(nr - f - 2, nr - 1);
     for (int u0 = 0; wave + nwaves * u0 < n; u0 += U) {
       // compaction of up to U rows
+      if constexpr (STAGED) {
+        // N <= 128: each row is two 64-entry pieces; the U rows' LDS reads are
+        // independent, so they are issued together (no per-row latency chain)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = wave + nwaves * (u0 + u);
+          const bool rv = i < n && alive[i < n ? i : 0];   // wave-uniform
+          int c = 0;
+#pragma unroll
+          for (int p0 = 0; p0 < 128; p0 += 64) {
+            const int p = p0 + lane;
+            const int e = (i < n ? i : 0) * n + p;
+            const bool ok = rv && p < n - 1 && alive[Js[p < n - 1 ? e : 0]];
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
+            const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
+            if (ok && c + pre < m) gw[u * GS + c + pre] = Ss[e];
+            c += __builtin_popcountll(bal);
+          }
+        }
+      } else {
 #pragma unroll 1
-      for (int u = 0; u < U; ++u) {
-        const int i = wave + nwaves * (u0 + u);
-        if (i >= n || !alive[i]) continue;   // wave-uniform
-        int c = 0;
-        for (int p0 = 0; p0 < n - 1 && c < m; p0 += 64) {
-          const int p = p0 + lane;
-          const int64_t e = static_cast<int64_t>(i) * n + p;
-          const bool ok = p < n - 1 && alive[STAGED ? Js[e] : Jg[e]];
-          const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
-          const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
-          if (ok && c + pre < m) gw[u * GS + c + pre] = STAGED ? Ss[e] : Sg[e];
-          c += __builtin_popcountll(bal);
+        for (int u = 0; u < U; ++u) {
+          const int i = wave + nwaves * (u0 + u);
+          if (i >= n || !alive[i]) continue;   // wave-uniform
+          int c = 0;
+          for (int p0 = 0; p0 < n - 1 && c < m; p0 += 64) {
+            const int p = p0 + lane;
+            const int64_t e = static_cast<int64_t>(i) * n + p;
+            const bool ok = p < n - 1 && alive[Jg[e]];
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
+            const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
+            if (ok && c + pre < m) gw[u * GS + c + pre] = Sg[e];
+            c += __builtin_popcountll(bal);
+          }
         }
       }
       __builtin_amdgcn_s_waitcnt(0);
@@ -312,7 +334,16 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
         float r = 0.f;
         if (m >= 8 && row_ok) {
           r = a[k_me];
-          for (int q = k_me + 8; q < n8; q += 8) r += a[q];
+          int q = k_me + 8;
+          // four loads in flight, added in the same sequential order
+          for (; q + 24 < n8; q += 32) {
+            const float x0 = a[q], x1 = a[q + 8], x2 = a[q + 16], x3 = a[q + 24];
+            r += x0;
+            r += x1;
+            r += x2;
+            r += x3;
+          }
+          for (; q < n8; q += 8) r += a[q];
         }
         const int g = lane & ~7;
         const float r1 = __shfl(r, g + 1), r2 = __shfl(r, g + 2), r3 = __shfl(r, g + 3);

@@ -26,6 +26,15 @@ import srfl_loader  # noqa: E402
 
 srfl_loader.load()
 
+# under pytest-xdist every worker would otherwise start a full-width BLAS pool:
+# the 4 oracle filter tests then take ~50x their serial time (oversubscription)
+if os.environ.get("PYTEST_XDIST_WORKER"):
+    try:
+        from threadpoolctl import threadpool_limits
+        threadpool_limits(max(1, (os.cpu_count() or 8) // int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "4"))))
+    except Exception:   # threadpoolctl missing: keep the default pools
+        pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
