@@ -1811,16 +1811,22 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
     double u_prev = 0.0;
     bool have_u = false;
 
-    for (int it = 0; it < iters; ++it) {
-      const long long t_it = dbg ? clock64() : 0;
-      if (DBG) clog_n = 0;
-      // ---- G back into registers; weights, g = G w, s = w^T G w
+    // G into registers (at the end of every iteration for the next one, as
+    // soon as M's last matvec has read them: the loads overlap the decision's
+    // reductions)
+    auto load_g = [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int c = 0; c < 32; ++c) {
         const double2 v = Gr[c];
         g[2 * c] = v.x;
         g[2 * c + 1] = v.y;
       }
+    };
+    load_g();
+    for (int it = 0; it < iters; ++it) {
+      const long long t_it = dbg ? clock64() : 0;
+      if (DBG) clog_n = 0;
+      // ---- weights, g = G w, s = w^T G w (G in registers)
       double o[4];
       reduce2(own && ai ? ci : 0.0, own && ai ? 1.0 : 0.0, o, 2);
       const double csum = o[0];
@@ -2064,6 +2070,7 @@ __global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
       if (own) xbuf[row] = ui;
       lds_barrier();
       const double mu_i = gmv();
+      if (it + 1 < iters) load_g();   // M is dead: G back for the next iteration
       const double cu = swi > 0.0 ? mu_i / swi : 0.0;
       const double ti = cu * cu / lam;
       if constexpr (MODE == 0) {
