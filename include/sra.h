@@ -390,7 +390,8 @@ int sra_apply_update_f64(const uint64_t* ptrs, const int64_t* seg, int32_t nseg,
 /* ---- k10: the DBA harness's Helper aggregators (src/DBA/helper.py) ---- */
 
 /* out[j] = s_k of column j (ascending, NaN anywhere -> NaN); k = (n-1)/2 is
- * torch.median's lower median (Helper.median, helper.py:529-569).  n <= 128. */
+ * torch.median's lower median (Helper.median, helper.py:529-569).  n <= 512
+ * (n > 128: an LDS bitonic sort per coordinate tile). */
 int sra_order_stat_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t k, float* out, void* stream);
 /* out = (sequential fp32 sum of the rows) / divisor, correctly rounded:
  * Helper.mom_krum's aliased bucket (helper.py:857-863, divisor count + 1) and

@@ -674,13 +674,64 @@ extern "C" int sra_trimmed_mean_f32(const float* X, int64_t n, int64_t d, int64_
 // DBA harness aggregates with (src/DBA/helper.py:561, :1025).  Runtime-N
 // register network (n <= 128); the kept slot s[k] is summed alone and divided
 // by 1, i.e. returned exactly.
+// Order statistic for 128 < N <= 512 (the DBA harness's torch.median lower
+// median, src/DBA/helper.py:561, with more clients): a tile of `tile`
+// coordinates x pn = next_pow2(N) slots in LDS ([slot][coordinate], so a
+// wave's compare-exchanges hit distinct banks), bitonic-sorted by the whole
+// workgroup in the NaN-last order of ce(); s[k], or NaN when the column holds
+// one (then slot N - 1 is NaN): torch.median's answer.
+constexpr int kOrderLdsFloats = 16384;   // 64 KiB tile
+__global__ void __launch_bounds__(256) order_stat_lds_kernel(const float* __restrict__ X, int n, int64_t d,
+                                                             int64_t ldx, int pn, int tile, int k,
+                                                             float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [pn][tile]
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * tile;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < pn * tile; e += blockDim.x) {
+    const int r = e / tile, c = e - r * tile;
+    const int64_t j = j0 + c;
+    lds[e] = (r < n && j < d) ? X[static_cast<int64_t>(r) * ldx + j] : qnan();
+  }
+  __syncthreads();
+  const int pairs = (pn / 2) * tile;
+  for (int kk = 2; kk <= pn; kk <<= 1) {
+    for (int st = kk >> 1; st > 0; st >>= 1) {
+      for (int q = tid; q < pairs; q += blockDim.x) {
+        const int c = q % tile;
+        const int h = q / tile;
+        const int i = ((h / st) * (2 * st)) + (h % st);
+        const int l = i + st;
+        float a = lds[i * tile + c], b = lds[l * tile + c];
+        if ((i & kk) == 0) ce(a, b); else ce(b, a);
+        lds[i * tile + c] = a;
+        lds[l * tile + c] = b;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid < tile) {
+    const int64_t j = j0 + tid;
+    if (j < d) out[j] = __builtin_isnan(lds[(n - 1) * tile + tid]) ? qnan() : lds[k * tile + tid];
+  }
+}
+
 extern "C" int sra_order_stat_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t k, float* out,
                                   void* stream) {
   int rc = check_matrix(X, n, d, ldx, out);
   if (rc) return rc;
-  SRA_REQUIRE(n <= 128, SRA_ERR_UNSUPPORTED, "order statistic supports N <= 128 (got %lld)", (long long)n);
+  SRA_REQUIRE(n <= 512, SRA_ERR_UNSUPPORTED, "order statistic supports N <= 512 (got %lld)", (long long)n);
   SRA_REQUIRE(k >= 0 && k < n, SRA_ERR_ARG, "order statistic k=%d out of [0, %lld)", k, (long long)n);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (n > 128) {
+    const int pn = next_pow2(static_cast<int>(n));
+    const int tile = kOrderLdsFloats / pn;
+    const size_t lds = sizeof(float) * static_cast<size_t>(pn) * tile;
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&order_stat_lds_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    hipLaunchKernelGGL(order_stat_lds_kernel, dim3(cdiv(d, tile)), dim3(256), lds, s, X, static_cast<int>(n), d, ldx,
+                       pn, tile, static_cast<int>(k), out);
+    return launch_status("order_stat_lds_kernel");
+  }
   const int P = static_cast<int>(cdiv(n, 16) * 16);
   const int64_t blocks = cdiv(d, 256);
 #define SRA_ORD(PP)                                                                                                  \

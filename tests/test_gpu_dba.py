@@ -206,7 +206,7 @@ def test_foolsgold(name):
 
 
 # ------------------------------------------------------------- k10 kernels
-@pytest.mark.parametrize("n", [1, 2, 3, 16, 17, 24, 33, 64, 100, 127, 128])
+@pytest.mark.parametrize("n", [1, 2, 3, 16, 17, 24, 33, 64, 100, 127, 128, 129, 200, 256, 257, 400, 512])
 def test_order_stat_all_k(n):
     rng = np.random.default_rng(n)
     x = rng.standard_normal((n, 1000)).astype(np.float32)
@@ -226,8 +226,15 @@ def test_order_stat_nan_and_strided():
     got = engine.order_stat(X[:, 1:2501], 19).cpu().numpy()
     np.testing.assert_array_equal(got, od.median(x[:, 1:2501]))
     assert np.isnan(got[9])
+    # N > 128: the LDS bitonic path, same semantics (NaN anywhere -> NaN)
+    y = rng.standard_normal((300, 2000)).astype(np.float32)
+    y[17, 5] = np.nan
+    Y = torch.from_numpy(y).to(DEV)
+    got = engine.order_stat(Y[:, 3:1990], 149).cpu().numpy()
+    np.testing.assert_array_equal(got, od.median(y[:, 3:1990]))
+    assert np.isnan(got[2])
     with pytest.raises(NotImplementedError):
-        engine.order_stat(torch.zeros((129, 8), device=DEV), 3)
+        engine.order_stat(torch.zeros((513, 8), device=DEV), 3)
 
 
 @pytest.mark.parametrize("d,off", [(4096, 0), (1001, 0), (4096, 1)])
