@@ -12,10 +12,10 @@ each rank reads only its N x d_r block:
   d-vector — no other data-path collective;
 * Krum (and the Krum rounds of Bulyan-Krum) needs the N x N client Gram: the
   centred Gram decomposes over columns (each column is centred by its own
-  mean), so each rank computes the Gram of its block and one all-reduce of
-  N*N fp64 (128 KiB at N=128) sums them; scoring is N-space work done
-  redundantly on every rank (identical inputs -> identical index), and the
-  chosen client's row is assembled with the same all-gather;
+  mean), so each rank computes the Gram of its block and one reduce of N*N
+  fp64 (128 KiB at N=128) sums them on rank 0, which alone scores the N x N
+  matrix (the score matrix stays on one GPU) and broadcasts the chosen
+  index(es); the chosen client's row is assembled with the same all-gather;
 * Bulyan's median / trimmed-mean selection rounds: one all-reduce of the
   <= N fp64 distance partials per round (the only per-round exchange), the
   pick made identically on every rank, then the local per-coordinate stage.
@@ -78,6 +78,22 @@ def coordinatewise(local_fn, X_shard, d, align=1, group=None):
     return gather_columns(local_fn(X_shard), d, align, group)
 
 
+def _gram_pick(G, pick, count, group=None):
+    """Sum the ranks' partial Grams on the group's first rank only, run
+    ``pick(G) -> (count,) int tensor`` there (the N x N scoring stays on one
+    GPU) and broadcast the indices; without a process group, pick(G)."""
+    if not dist.is_initialized():
+        return pick(G)
+    _, rank = _world(group)
+    root = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.reduce(G, dst=root, op=dist.ReduceOp.SUM, group=group)
+    idx = torch.zeros(count, dtype=torch.int64, device=G.device)
+    if rank == 0:
+        idx.copy_(torch.as_tensor(pick(G), device=G.device).reshape(count).to(torch.int64))
+    dist.broadcast(idx, src=root, group=group)
+    return idx
+
+
 def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
     """Krum over a column-sharded layer.
 
@@ -85,9 +101,8 @@ def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
     select_fn(G, f) -> index of the chosen client (from the full Gram).
     Returns (full row of the chosen client, index)."""
     G = gram_fn(X_shard).to(torch.float64).contiguous()
-    if dist.is_initialized():   # (a 1-rank group still goes through the collective)
-        dist.all_reduce(G, op=dist.ReduceOp.SUM, group=group)
-    idx = int(select_fn(G, f))
+    # (a 1-rank group still goes through the collectives)
+    idx = int(_gram_pick(G, lambda g: torch.tensor([int(select_fn(g, f))]), 1, group)[0])
     row = gather_columns(X_shard[idx], d, align, group)
     return row, idx
 
@@ -97,15 +112,14 @@ def mom_krum(ops, X_shard, d, f, bucket_size=3, group=None, align=1):
 
     The centred Gram of the bucket means decomposes over columns like Krum's:
     each rank forms its partial from its own columns without writing the means
-    (``ops["gram_buckets"]``), one all-reduce of B x B doubles sums them, every
-    rank picks the same bucket (``ops["krum_select"]``), and the bucket's mean
+    (``ops["gram_buckets"]``), one reduce of B x B doubles sums them on the
+    first rank, which picks the bucket (``ops["krum_select"]``) and broadcasts
+    it, and the bucket's mean
     over each rank's columns (``ops["bucket_mean"]``, np.mean order) is
     all-gathered.  Returns (full mean row of the chosen bucket, bucket index)."""
     n = int(X_shard.shape[0])
     G = ops["gram_buckets"](X_shard, bucket_size).to(torch.float64).contiguous()
-    if dist.is_initialized():
-        dist.all_reduce(G, op=dist.ReduceOp.SUM, group=group)
-    idx = int(ops["krum_select"](G, f))
+    idx = int(_gram_pick(G, lambda g: torch.tensor([int(ops["krum_select"](g, f))]), 1, group)[0])
     lo = idx * bucket_size
     part = ops["bucket_mean"](X_shard[lo:min(lo + bucket_size, n)])
     return gather_columns(part, d, align, group), idx
@@ -119,8 +133,9 @@ def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
     and the distances over its own columns (``ops["bulyan_round"]``), one
     all-reduce of <= N fp64 partials per round sums them, and every rank
     makes the same pick (``ops["bulyan_pick"]``) from the identical sums.
-    Krum mode: one all-reduce of the partial centred Gram, then the theta
-    Krum rounds redundantly on every rank (``ops["krum_rounds"]``).  The
+    Krum mode: one reduce of the partial centred Gram to the first rank, which
+    runs the theta Krum rounds (``ops["krum_rounds"]``) and broadcasts the
+    order.  The
     per-coordinate stage is local (``ops["bulyan_stage"]``) and one all-gather
     assembles the (d,) float64 result.
 
@@ -137,9 +152,7 @@ def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
     on = dist.is_initialized()   # (a 1-rank group still goes through the collectives)
     if aggsubfunc == "krum":
         G = ops["gram"](X_shard).to(torch.float64).contiguous()
-        if on:
-            dist.all_reduce(G, op=dist.ReduceOp.SUM, group=group)
-        order = ops["krum_rounds"](G, int(f), theta)
+        order = _gram_pick(G, lambda g: ops["krum_rounds"](g, int(f), theta), theta, group)
         S = X_shard.index_select(0, order.to(torch.long)).contiguous()
     else:
         if aggsubfunc not in ("median", "trimmedmean"):
