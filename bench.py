@@ -450,8 +450,9 @@ def main():
     full = torch.empty(d * world, dtype=odt, device=device) if world > 1 else None
     fn = AGG[a.agg]
     # N>1, Krum / Bulyan: the selection is global -- the sharded forms exchange
-    # the N x N Gram (one all-reduce) or, per Bulyan round, the <= N distance
-    # partials (one all-reduce each), then assemble the (d*world,) result
+    # the N x N Gram (one reduce to the scoring rank, the pick broadcast) or,
+    # per Bulyan round, the <= N distance partials (one all-reduce each), then
+    # assemble the (d*world,) result
     sharded = None
     if world > 1 and a.agg in ("krum", "mom_krum", "bulyankrum", "bulyanmedian", "bulyantrimmedmean"):
         ops = shard.engine_ops()
@@ -563,7 +564,7 @@ def main():
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
                    "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, d // block)
                                    if pipelined else
-                                   ("d-shard x%d, all-reduced selection" % world if sharded is not None
+                                   ("d-shard x%d, reduced selection" % world if sharded is not None
                                     else "d-shard x%d" % world))},
         "roofline": {"bound": bound, "kernel": kernel_label(a.agg, n), "achieved": round(achieved, 2),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
