@@ -91,7 +91,7 @@ int sra_gram_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
  * so ||x_i - x_j||^2 = G_ii + G_jj - 2 G_ij.  bf16 MFMA on an exact three-way
  * split of every centred fp32 value (six products per term: fp32-product
  * accuracy), fp32 partials per k-group, fp64 reduction.
- * 1 <= n <= 512 (n > 256: one launch per pair of 128-client blocks, all
+ * 1 <= n <= 8192 (n > 256: one launch per pair of 128-client blocks, all
  * centred by the fp32 mean over the n clients).  Feeds krum_
  * (src/robust_estimator.py:234-244). */
 int sra_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes,
@@ -109,12 +109,17 @@ int sra_krum_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
  *  scores (optional, n floats) receive round 0's scores = krum_'s metric.
  *  Distances: from the centred Gram for d > 1024; for d <= 1024, or data with
  *  a NaN / inf, each pair's fp32 difference squared and summed in fp64 (the
- *  reference's np.linalg.norm of the difference, :242). */
+ *  reference's np.linalg.norm of the difference, :242).  1 <= n <= 8192
+ *  (n > 512: the rounds compact each row through a global scratch). */
 int sra_krum_select_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t rounds,
                         int32_t* order, float* scores, void* ws, size_t ws_bytes, void* stream);
 
+/* Workspace for sra_krum_from_gram, in bytes (12*n*n, plus the rounds'
+ * scratch for n > 512). */
+int sra_krum_from_gram_workspace_bytes(int64_t n, size_t* bytes);
+
 /* Same selection from a precomputed Gram G (e.g. summed over GPUs);
- * ws >= 12*n*n bytes. */
+ * ws from sra_krum_from_gram_workspace_bytes. */
 int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t rounds, int32_t* order, float* scores,
                        void* ws, size_t ws_bytes, void* stream);
 
@@ -390,7 +395,7 @@ int sra_apply_update_f64(const uint64_t* ptrs, const int64_t* seg, int32_t nseg,
 /* ---- k10: the DBA harness's Helper aggregators (src/DBA/helper.py) ---- */
 
 /* out[j] = s_k of column j (ascending, NaN anywhere -> NaN); k = (n-1)/2 is
- * torch.median's lower median (Helper.median, helper.py:529-569).  n <= 512
+ * torch.median's lower median (Helper.median, helper.py:529-569).  n <= 16384
  * (n > 128: an LDS bitonic sort per coordinate tile). */
 int sra_order_stat_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t k, float* out, void* stream);
 /* out = (sequential fp32 sum of the rows) / divisor, correctly rounded:

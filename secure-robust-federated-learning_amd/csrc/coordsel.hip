@@ -674,7 +674,7 @@ extern "C" int sra_trimmed_mean_f32(const float* X, int64_t n, int64_t d, int64_
 // DBA harness aggregates with (src/DBA/helper.py:561, :1025).  Runtime-N
 // register network (n <= 128); the kept slot s[k] is summed alone and divided
 // by 1, i.e. returned exactly.
-// Order statistic for 128 < N <= 512 (the DBA harness's torch.median lower
+// Order statistic for 128 < N <= 16384 (the DBA harness's torch.median lower
 // median, src/DBA/helper.py:561, with more clients): a tile of `tile`
 // coordinates x pn = next_pow2(N) slots in LDS ([slot][coordinate], so a
 // wave's compare-exchanges hit distinct banks), bitonic-sorted by the whole
@@ -719,7 +719,8 @@ extern "C" int sra_order_stat_f32(const float* X, int64_t n, int64_t d, int64_t 
                                   void* stream) {
   int rc = check_matrix(X, n, d, ldx, out);
   if (rc) return rc;
-  SRA_REQUIRE(n <= 512, SRA_ERR_UNSUPPORTED, "order statistic supports N <= 512 (got %lld)", (long long)n);
+  SRA_REQUIRE(n <= kOrderLdsFloats, SRA_ERR_UNSUPPORTED, "order statistic supports N <= %d (got %lld)",
+              kOrderLdsFloats, (long long)n);
   SRA_REQUIRE(k >= 0 && k < n, SRA_ERR_ARG, "order statistic k=%d out of [0, %lld)", k, (long long)n);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (n > 128) {

@@ -560,7 +560,7 @@ int launch_gram_buckets(const float* X, int n, int bs, int64_t d, int64_t ldx, d
   }
 }
 
-constexpr int kGramMaxClients = 512;
+constexpr int kGramMaxClients = 8192;   // N > 512: pairs of 128-client blocks (Krum without a client ceiling)
 constexpr int kGramPairRows = 128;
 
 size_t gram_workspace_bytes(int n, int64_t d) {

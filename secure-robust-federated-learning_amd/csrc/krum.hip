@@ -131,18 +131,20 @@ __global__ void __launch_bounds__(256) krum_direct_kernel(const float* __restric
 // Sort every row's off-diagonal distances ascending (ties by j): one workgroup
 // per row, bitonic network in LDS over next_pow2(n-1) slots.  With the exact
 // route flagged, the distances come from acc instead of D.
+// Dynamic LDS: next_pow2(n - 1) (value, index) pairs, at most 64 KiB.
 __global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restrict__ D, int n,
                                                            float* __restrict__ S, int* __restrict__ J,
                                                            const int* __restrict__ nonfinite,
                                                            const double* __restrict__ acc,
                                                            const int* __restrict__ cls) {
-  __shared__ float kv[kMaxClients];
-  __shared__ int kj[kMaxClients];
+  extern __shared__ __attribute__((aligned(16))) char rs_smem[];
   const int i = blockIdx.x;
   const int m = n - 1;
   const bool direct = nonfinite != nullptr && *nonfinite != 0;
   int pn = 1;
   while (pn < m) pn <<= 1;
+  float* kv = reinterpret_cast<float*>(rs_smem);
+  int* kj = reinterpret_cast<int*>(kv + pn);
   for (int p = threadIdx.x; p < pn; p += blockDim.x) {
     if (p < m) {
       const int j = p < i ? p : p + 1;
@@ -411,6 +413,111 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
   }
 }
 
+// numpy's pairwise fp32 sum over one wave for any n the split depth reaches:
+// each split leaves pieces of at most n/2 + 8 elements, so DEPTH levels cover
+// n <= 128 * 2^DEPTH - 16 (DEPTH = 7: n <= 16368).  Out of line, one copy per
+// level.
+template <int DEPTH>
+__device__ __attribute__((noinline)) float wave_pairwise_deep_f32(const float* a, int n) {
+  if constexpr (DEPTH == 0) {
+    return wave_pw_block_f32(a, n);
+  } else {
+    if (n <= 128) return wave_pw_block_f32(a, n);
+    int q = n / 2;
+    q -= q % 8;
+    const float lo = wave_pairwise_deep_f32<DEPTH - 1>(a, q);
+    return lo + wave_pairwise_deep_f32<DEPTH - 1>(a + q, n - q);
+  }
+}
+
+// Krum rounds for kMaxClients < N <= kKrumMaxClients (no client-count ceiling
+// the shipped configurations reach; the reference has none,
+// robust_estimator.py:234-249).  One workgroup of 16 waves; alive flags and
+// scores in dynamic LDS; a wave takes one alive row at a time, compacts its
+// first m alive sorted distances into its own slice of the global scratch
+// (16 x n floats, L2-resident) and sums them in numpy's pairwise order.
+constexpr int kKrumMaxClients = 8192;
+__global__ void __launch_bounds__(1024) krum_rounds_huge_kernel(const float* __restrict__ Sg,
+                                                                const int* __restrict__ Jg, int n, int f, int rounds,
+                                                                int* __restrict__ order, float* __restrict__ scores0,
+                                                                float* __restrict__ scratch) {
+  extern __shared__ __attribute__((aligned(16))) char kh_smem[];
+  float* score = reinterpret_cast<float*>(kh_smem);
+  unsigned char* alive = reinterpret_cast<unsigned char*>(score + n);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int nwaves = blockDim.x >> 6;
+  float* gw = scratch + static_cast<int64_t>(wave) * n;
+  for (int i = tid; i < n; i += blockDim.x) alive[i] = 1;
+  __syncthreads();
+  for (int t = 0; t < rounds; ++t) {
+    const int nr = n - t;
+    const int m = slice_count(nr - f - 2, nr - 1);
+#pragma unroll 1
+    for (int i = wave; i < n; i += nwaves) {
+      if (!alive[i]) continue;   // wave-uniform
+      int c = 0;
+      for (int p0 = 0; p0 < n - 1 && c < m; p0 += 64) {
+        const int p = p0 + lane;
+        const int64_t e = static_cast<int64_t>(i) * n + p;
+        const bool ok = p < n - 1 && alive[checked_row(Jg[p < n - 1 ? e : 0], n)];
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
+        const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
+        if (ok && c + pre < m) gw[c + pre] = Sg[e];
+        c += __builtin_popcountll(bal);
+      }
+      __threadfence_block();
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      const float v = wave_pairwise_deep_f32<7>(gw, m);
+      if (lane == 0) score[i] = v;
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (wave == 0) {
+      // np.argmin as krum_rounds_kernel: first minimum, a NaN is the minimum
+      int bc = 2, bi = 0x7fffffff;
+      float bv = 0.f;
+      for (int i = lane; i < n; i += 64) {
+        const float v = score[i];
+        const int c = !alive[i] ? 2 : (v != v ? 0 : 1);
+        if (c < bc || (c == bc && c == 1 && v < bv)) {
+          bc = c;
+          bv = v;
+          bi = i;
+        }
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const int oc = __shfl_xor(bc, off);
+        const float ov = __shfl_xor(bv, off);
+        const int oi = __shfl_xor(bi, off);
+        const bool better = oc < bc || (oc == bc && ((oc == 1 && ov < bv) || ((oc != 1 || ov == bv) && oi < bi)));
+        if (better) {
+          bc = oc;
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (lane == 0) {
+        const int best = bc < 2 ? bi : -1;
+        order[t] = best;
+        if (best >= 0) alive[best] = 0;
+      }
+    }
+    if (t == 0 && scores0) {
+      for (int i = tid; i < n; i += blockDim.x) scores0[i] = score[i];
+    }
+    __syncthreads();
+  }
+}
+
+// bytes of the rounds' compaction scratch (N > kMaxClients only)
+static size_t krum_scratch_bytes(int n) { return n > kMaxClients ? static_cast<size_t>(16) * n * 4 + 256 : 0; }
+
 unsigned int krum_row_faults(bool reset) { return tu_row_faults(reset); }
 
 // out[r, :] = X[order[r], :] (the chosen clients' rows); the index is checked
@@ -428,10 +535,11 @@ size_t krum_workspace_bytes(int n, int64_t d);
 size_t gram_workspace_bytes(int n, int64_t d);
 int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes, hipStream_t s);
 
-// workspace layout: [flag (256 B)][G fp64 n*n][acc fp64 n*n][cls int n*n][D n*n][S n*n][J n*n][gram slab]
+// workspace layout: [flag (256 B)][G fp64 n*n][acc fp64 n*n][cls int n*n][D n*n][S n*n][J n*n]
+// [rounds scratch (N > kMaxClients)][gram slab]
 size_t krum_workspace_bytes(int n, int64_t d) {
   const size_t nn = static_cast<size_t>(n) * n;
-  return 256 + nn * 8 * 2 + nn * 4 * 4 + gram_workspace_bytes(n, d);
+  return 256 + nn * 8 * 2 + nn * 4 * 4 + krum_scratch_bytes(n) + gram_workspace_bytes(n, d);
 }
 
 // X (optional): the data G came from; with it, a non-finite G switches the
@@ -464,10 +572,24 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
     if (rc) return rc;
   }
   if (n > 1) {
-    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), 0, s, D, n, S, J, X ? nonfinite : nullptr,
+    int pn = 1;
+    while (pn < n - 1) pn <<= 1;
+    static const hipError_t attr_s =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(krum_rowsort_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 8 * kKrumMaxClients);
+    SRA_REQUIRE(attr_s == hipSuccess || pn * 8 <= 65536, SRA_ERR_UNSUPPORTED,
+                "krum_rowsort_kernel: cannot reserve %d bytes of dynamic LDS", pn * 8);
+    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), pn * 8, s, D, n, S, J, X ? nonfinite : nullptr,
                        X ? acc : nullptr, X ? cls : nullptr);
     rc = launch_status("krum_rowsort_kernel");
     if (rc) return rc;
+  }
+  if (n > kMaxClients) {
+    float* scratch = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(J + nn) + 255) & ~uintptr_t(255));
+    const int lds = n * 5 + 16;   // scores + alive flags
+    hipLaunchKernelGGL(krum_rounds_huge_kernel, dim3(1), dim3(1024), lds, s, S, J, n, f, rounds, order, scores0,
+                       scratch);
+    return launch_status("krum_rounds_huge_kernel");
   }
   if (n <= 128) {
     const int lds = 16 * 8 * kKrumGStaged * 4 + n * n * 5;   // compacted rows + S fp32 + J bytes
@@ -502,6 +624,9 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
   return launch_status("krum_rounds_kernel");
 }
 
+// [D n*n][S n*n][J n*n][rounds scratch]
+size_t krum_from_gram_workspace_bytes(int n) { return static_cast<size_t>(n) * n * 12 + krum_scratch_bytes(n); }
+
 int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int* order, float* scores0,
                                  char* ws, hipStream_t s) {
   return launch_krum_rounds(G, n, f, rounds, order, scores0, ws, nullptr, 0, 0, nullptr, nullptr, nullptr, s);
@@ -509,7 +634,8 @@ int launch_krum_rounds_from_gram(const double* G, int n, int f, int rounds, int*
 
 int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds, int* order, float* scores0,
                 void* ws, size_t ws_bytes, hipStream_t s) {
-  SRA_REQUIRE(n >= 1 && n <= kMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d (got %d)", kMaxClients, n);
+  SRA_REQUIRE(n >= 1 && n <= kKrumMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d (got %d)",
+              kKrumMaxClients, n);
   SRA_REQUIRE(rounds >= 1 && rounds <= n, SRA_ERR_ARG, "rounds must be in [1, N] (got %d)", rounds);
   SRA_REQUIRE(ws != nullptr && ws_bytes >= krum_workspace_bytes(n, d), SRA_ERR_WORKSPACE,
               "Krum workspace too small: need %zu bytes", krum_workspace_bytes(n, d));
@@ -520,7 +646,7 @@ int launch_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int rounds
   double* acc = G + nn;
   int* cls = reinterpret_cast<int*>(acc + nn);
   char* rest = reinterpret_cast<char*>(cls + nn);
-  char* slab = rest + nn * 4 * 3;
+  char* slab = rest + nn * 4 * 3 + krum_scratch_bytes(n);
   int rc = launch_gram(X, n, d, ldx, G, slab, gram_workspace_bytes(n, d), s);
   if (rc) return rc;
   return launch_krum_rounds(G, n, f, rounds, order, scores0, rest, X, d, ldx, nonfinite, acc, cls, s);
@@ -557,7 +683,7 @@ int launch_mom_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int bs
   double* acc = G + nn;
   int* cls = reinterpret_cast<int*>(acc + nn);
   char* rest = reinterpret_cast<char*>(cls + nn);
-  float* slab = reinterpret_cast<float*>(rest + nn * 4 * 3);
+  float* slab = reinterpret_cast<float*>(rest + nn * 4 * 3 + krum_scratch_bytes(nb));
   int rc = launch_gram_buckets(X, n, bs, d, ldx, G, slab, s);
   if (rc) return rc;
   rc = launch_krum_rounds(G, nb, f, 1, order, nullptr, rest, X, d, ldx, nonfinite, acc, cls, s, n, bs);
@@ -589,8 +715,16 @@ extern "C" int sra_mom_krum_f32(const float* X, int64_t n, int64_t d, int64_t ld
 
 extern "C" int sra_krum_workspace_bytes(int64_t n, int64_t d, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
-  SRA_REQUIRE(n >= 1 && n <= kMaxClients && d >= 1, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kMaxClients);
+  SRA_REQUIRE(n >= 1 && n <= kKrumMaxClients && d >= 1, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d",
+              kKrumMaxClients);
   *bytes = krum_workspace_bytes(static_cast<int>(n), d);
+  return SRA_OK;
+}
+
+extern "C" int sra_krum_from_gram_workspace_bytes(int64_t n, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && n <= kKrumMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kKrumMaxClients);
+  *bytes = krum_from_gram_workspace_bytes(static_cast<int>(n));
   return SRA_OK;
 }
 
@@ -605,9 +739,10 @@ extern "C" int sra_krum_select_f32(const float* X, int64_t n, int64_t d, int64_t
 extern "C" int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t rounds, int32_t* order,
                                   float* scores, void* ws, size_t ws_bytes, void* stream) {
   SRA_REQUIRE(G != nullptr && order != nullptr && ws != nullptr, SRA_ERR_ARG, "null pointer");
-  SRA_REQUIRE(n >= 1 && n <= kMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kMaxClients);
+  SRA_REQUIRE(n >= 1 && n <= kKrumMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kKrumMaxClients);
   SRA_REQUIRE(rounds >= 1 && rounds <= n, SRA_ERR_ARG, "rounds must be in [1, N]");
-  SRA_REQUIRE(ws_bytes >= static_cast<size_t>(n) * n * 12, SRA_ERR_WORKSPACE, "workspace too small");
+  SRA_REQUIRE(ws_bytes >= krum_from_gram_workspace_bytes(static_cast<int>(n)), SRA_ERR_WORKSPACE,
+              "workspace too small: need %zu bytes", krum_from_gram_workspace_bytes(static_cast<int>(n)));
   return launch_krum_rounds_from_gram(G, static_cast<int>(n), f, rounds, order, scores, static_cast<char*>(ws),
                                       static_cast<hipStream_t>(stream));
 }

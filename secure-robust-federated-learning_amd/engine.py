@@ -122,9 +122,10 @@ def krum_from_gram(G, f, rounds=1, scores=True):
     n = int(G.shape[0])
     order = torch.empty(rounds, dtype=torch.int32, device=G.device)
     sc = torch.empty(n, dtype=torch.float32, device=G.device) if scores else None
-    ws = _workspace(12 * n * n, G.device)
+    nb = _lib.query_bytes("sra_krum_from_gram_workspace_bytes", n)
+    ws = _workspace(nb, G.device)
     _lib.call("sra_krum_from_gram", G.contiguous().data_ptr(), n, int(f), int(rounds), order.data_ptr(),
-              sc.data_ptr() if sc is not None else None, ws.data_ptr(), 12 * n * n, _stream_ptr(G.device))
+              sc.data_ptr() if sc is not None else None, ws.data_ptr(), nb, _stream_ptr(G.device))
     return order, sc
 
 

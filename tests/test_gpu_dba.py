@@ -233,8 +233,16 @@ def test_order_stat_nan_and_strided():
     got = engine.order_stat(Y[:, 3:1990], 149).cpu().numpy()
     np.testing.assert_array_equal(got, od.median(y[:, 3:1990]))
     assert np.isnan(got[2])
+    # N > 512 (no ceiling below the reference's, helper.py:561): 16 / 2 / 1
+    # coordinates per 64 KiB tile
+    for n in (513, 1000, 9000):
+        z = rng.standard_normal((n, 37)).astype(np.float32)
+        z[n // 2, 7] = np.nan
+        got = engine.order_stat(torch.from_numpy(z).to(DEV), (n - 1) // 2).cpu().numpy()
+        np.testing.assert_array_equal(got, od.median(z))
+        assert np.isnan(got[7])
     with pytest.raises(NotImplementedError):
-        engine.order_stat(torch.zeros((513, 8), device=DEV), 3)
+        engine.order_stat(torch.zeros((16385, 8), device=DEV), 3)
 
 
 @pytest.mark.parametrize("d,off", [(4096, 0), (1001, 0), (4096, 1)])

@@ -160,3 +160,50 @@ def test_bulyan_krum_many_clients(n, f):
     _, removed = orc.bulyan_select(list(x), f, "krum")
     _, sel = engine.bulyan(torch.from_numpy(x).cuda(), f, "krum", selected=True)
     assert sel.cpu().tolist() == removed
+
+
+@pytest.mark.parametrize("n,f,d", [(600, 20, 3000), (1024, 100, 2000), (1100, 3, 2000), (2100, 40, 64)])
+def test_krum_beyond_512_clients(n, f, d):
+    """No client ceiling the reference lacks (robust_estimator.py:234-249 has
+    none): N > 512 takes the pair Gram over 128-client blocks, the dynamic-LDS
+    row sorts and the global-scratch rounds (krum_rounds_huge_kernel).
+    m = 1095 (N = 1100, f = 3) needs four split levels of numpy's pairwise sum;
+    d = 64 is the exact per-pair route."""
+    x = make_rows(n, d, seed=310 + n, byz=min(f, n // 3))
+    want = orc.krum_(list(x), f)
+    order, scores = engine.krum_select(torch.from_numpy(x).cuda(), f, 1)
+    assert int(order.cpu()[0]) == int(np.argmin(want))
+    np.testing.assert_allclose(scores.cpu().numpy(), np.array(want, np.float32), rtol=SCORE_RTOL)
+
+
+@pytest.mark.parametrize("n,f,d,rounds", [(700, 30, 3000, 6), (1500, 50, 128, 4)])
+def test_krum_rounds_beyond_512_clients(n, f, d, rounds):
+    """Bulyan-Krum-style rounds (delete the pick, re-score the rest with f
+    fixed, robust_estimator.py:289-296) at N > 512, from the data and from the
+    Gram (krum_from_gram, the sharded route's entry)."""
+    x = make_rows(n, d, seed=410 + n, byz=f // 2)
+    dist = orc.pairwise_l2(list(x))
+    alive = list(range(n))
+    want = []
+    for _ in range(rounds):
+        sc = orc.krum_scores_from_dist(dist[np.ix_(alive, alive)], f)
+        want.append(alive.pop(int(np.argmin(sc))))
+    X = torch.from_numpy(x).cuda()
+    order, _ = engine.krum_select(X, f, rounds, scores=False)
+    assert order.cpu().tolist() == want
+    if d > 1024:
+        order_g, _ = engine.krum_from_gram(engine.gram(X), f, rounds, scores=False)
+        assert order_g.cpu().tolist() == want
+
+
+def test_gram_beyond_512_clients():
+    """The pair Gram at N = 1000 (8 blocks, 28 pair launches) against fp64."""
+    n, d = 1000, 2500
+    x = make_rows(n, d, seed=77, byz=5)
+    G = engine.gram(torch.from_numpy(x).cuda()).cpu().numpy()
+    xc = x.astype(np.float64)
+    xc -= xc.mean(axis=0)
+    gc = xc @ xc.T
+    d2 = np.maximum(np.diag(gc)[:, None] + np.diag(gc)[None, :] - 2 * gc, 0.0)
+    got = np.diag(G)[:, None] + np.diag(G)[None, :] - 2 * G
+    np.testing.assert_allclose(got, d2, rtol=2e-5, atol=1e-9 * d2.max())
