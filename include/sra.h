@@ -176,8 +176,9 @@ int sra_bulyan_workspace_bytes(int64_t n, int64_t d, int32_t f, int32_t mode, si
  * stream-ordered): 1 if a median / trimmed-mean round found no strict
  * minimum distance -- every distance NaN / inf, where the reference's
  * `assert min_index != None` (:308, :321) raises -- else 0.  theta <= 0 ->
- * SRA_ERR_THETA.  1 <= n <= 512 (more than 128 remaining clients: LDS k-select + distance
- * passes per round; theta > 128: an LDS-sorted per-coordinate stage). */
+ * SRA_ERR_THETA.  1 <= n <= 8192 (more than 128 remaining clients: LDS k-select + distance
+ * passes per round, the distances in groups of 1024 rows above 512; theta > 128: an
+ * LDS-sorted per-coordinate stage, 64 coordinates per tile up to theta = 512, fewer above). */
 int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f, int32_t mode, double* out,
                    int32_t* selected, int32_t* status, void* ws, size_t ws_bytes, void* stream);
 
@@ -189,7 +190,7 @@ int sra_bulyan_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t f,
  * harness's lower median, src/DBA/helper.py:1025) of the listed rows; dist[r]
  * (nr doubles) = squared L2 distance of listed row r to agg over this block's
  * columns.  Column shards' dist vectors sum to the full distance (up to fp64
- * rounding: the per-tile partials are associated differently).  N <= 512
+ * rounding: the per-tile partials are associated differently).  N <= 8192
  * (rounds with more than 128 listed rows take an LDS k-select + distance pass);
  * workspace from sra_bulyan_round_workspace_bytes (sized by the block's d). */
 int sra_bulyan_round_workspace_bytes(int64_t n, int64_t d, size_t* bytes);
@@ -206,7 +207,7 @@ int sra_bulyan_pick(const double* dist, const int32_t* rows, int32_t nr, int32_t
  * i-th selected vector in selection order, row stride lds): out[j] (float64)
  * as sra_bulyan_f32's final stage computes it for robust_estimator.py:324-330
  * (bulyan_one_coordinate over np_grads[:, j], beta = theta - 2f, Python slice
- * semantics for beta < 0).  1 <= theta <= 512; workspace from
+ * semantics for beta < 0).  1 <= theta <= 8192; workspace from
  * sra_bulyan_stage_workspace_bytes (8 d bytes plus a few hundred). */
 int sra_bulyan_stage_workspace_bytes(int64_t theta, int64_t d, size_t* bytes);
 int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, int64_t lds, int32_t beta, double* out,

@@ -318,8 +318,9 @@ __global__ void __launch_bounds__(256) bulyan_pick_kernel(const double* __restri
 //     whichever path a round took.
 // Row indices are clamped to the matrix (a bad list cannot fault).
 // ---------------------------------------------------------------------------
-constexpr int kBigMaxClients = 512;
+constexpr int kBigMaxClients = 8192;   // as Krum (krum.hip kKrumMaxClients)
 constexpr int kBigLdsFloats = 16384;   // 64 KiB tile
+constexpr int kDistRowGroup = 1024;    // dist_rows_kernel<4>: rows per launch above 512
 
 __global__ void __launch_bounds__(256) select_rows_lds_kernel(const float* __restrict__ X, int64_t ldx,
                                                               const int* __restrict__ rows, int nrows_x, int n, int pn,
@@ -861,7 +862,8 @@ __global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(cons
 }
 
 // ---------------------------------------------------------------------------
-// The stage for theta in (128, kBigMaxClients]: a 64-coordinate tile of pn =
+// The stage for theta in (128, kBigMaxClients]: a TW-coordinate tile (TW = 64
+// up to theta = 512, halved with every doubling of pn above) of pn =
 // next_pow2(theta) slots in LDS per 256-thread block, filled in selection
 // order through the row list, bitonic-sorted by the block; then one lane per
 // coordinate runs the register kernel's logic on its sorted column: the
@@ -872,24 +874,27 @@ __global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(cons
 // global memory).  NaN / inf columns and inexact ones are listed for
 // bulyan_listed_big_kernel (the stage by definition).
 // ---------------------------------------------------------------------------
+template <int TW>
 __global__ void __launch_bounds__(256) bulyan_final_lds_kernel(const float* __restrict__ S, int64_t lds_,
                                                                const int* __restrict__ rows, int nrows_s, int theta,
                                                                int pn, int keep, int64_t d, double* __restrict__ out,
                                                                int* __restrict__ nf_count,
                                                                int64_t* __restrict__ nf_list) {
-  extern __shared__ __attribute__((aligned(16))) float colt[];   // [pn][64]
+  static_assert(TW >= 1 && TW <= 64 && (TW & (TW - 1)) == 0, "tile width: a power of two <= 64");
+  constexpr int LG = __builtin_ctz(TW);
+  extern __shared__ __attribute__((aligned(16))) float colt[];   // [pn][TW]
   __shared__ unsigned mnb_s[64], mxb_s[64];
   __shared__ int nonfin_s[64];
   const int tid = threadIdx.x;
-  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * TW;
   if (tid < 64) {
     mnb_s[tid] = 0xffffffffu;
     mxb_s[tid] = 0u;
     nonfin_s[tid] = 0;
   }
   __syncthreads();
-  for (int e = tid; e < pn * 64; e += blockDim.x) {
-    const int p = e >> 6, c = e & 63;
+  for (int e = tid; e < pn * TW; e += blockDim.x) {
+    const int p = e >> LG, c = e & (TW - 1);
     const int64_t j = j0 + c;
     float x = __builtin_inff();
     if (p < theta && j < d) {
@@ -906,23 +911,23 @@ __global__ void __launch_bounds__(256) bulyan_final_lds_kernel(const float* __re
     colt[e] = x;
   }
   __syncthreads();
-  const int pairs = (pn / 2) * 64;
+  const int pairs = (pn / 2) * TW;
   for (int k = 2; k <= pn; k <<= 1) {
     for (int s = k >> 1; s > 0; s >>= 1) {
       for (int q = tid; q < pairs; q += blockDim.x) {
-        const int c = q & 63;
-        const int h = q >> 6;
+        const int c = q & (TW - 1);
+        const int h = q >> LG;
         const int i = ((h / s) * (2 * s)) + (h % s);
         const int l = i + s;
-        float a = colt[i * 64 + c], b = colt[l * 64 + c];
+        float a = colt[i * TW + c], b = colt[l * TW + c];
         if ((i & k) == 0) ce(a, b); else ce(b, a);
-        colt[i * 64 + c] = a;
-        colt[l * 64 + c] = b;
+        colt[i * TW + c] = a;
+        colt[l * TW + c] = b;
       }
       __syncthreads();
     }
   }
-  if (tid >= 64) return;
+  if (tid >= TW) return;
   const int64_t j = j0 + tid;
   if (j >= d) return;
   if (keep == 0) {   // the mean of an empty slice
@@ -946,7 +951,7 @@ __global__ void __launch_bounds__(256) bulyan_final_lds_kernel(const float* __re
     nf_list[atomicAdd(nf_count, 1)] = 2 * j;
     return;
   }
-  auto s = [&](int p) -> float { return colt[p * 64 + tid]; };
+  auto s = [&](int p) -> float { return colt[p * TW + tid]; };
   const bool even = (theta & 1) == 0;
   const int pl = even ? theta / 2 - 1 : (theta - 1) / 2;
   const float cl = s(pl), cu = s(theta / 2);
@@ -968,23 +973,25 @@ __global__ void __launch_bounds__(256) bulyan_final_lds_kernel(const float* __re
 }
 
 // Listed columns of the big stage: the stage by definition
-// (bulyan_stage_generic), one lane per column, the rank map in LDS.
+// (bulyan_stage_generic), one lane per column, the rank map in LDS
+// ([theta][blockDim.x]: 32 lanes up to theta = 1024, fewer above).
 __global__ void __launch_bounds__(32) bulyan_listed_big_kernel(const float* __restrict__ S, int64_t lds_,
                                                                const int* __restrict__ rows, int nrows_s, int theta,
                                                                int keep, const int* __restrict__ nf_count,
                                                                const int64_t* __restrict__ nf_list,
                                                                double* __restrict__ out) {
-  extern __shared__ int rank_slots[];   // [theta][32]
+  extern __shared__ int rank_slots[];   // [theta][L]
   const int t = threadIdx.x;
+  const int L = blockDim.x;
   const int cnt = *nf_count;
-  for (int e = blockIdx.x * 32 + t; e < cnt; e += gridDim.x * 32) {
+  for (int e = blockIdx.x * L + t; e < cnt; e += gridDim.x * L) {
     const int64_t j = nf_list[e] >> 1;
     auto a = [&](int i) -> double {
       return S[static_cast<int64_t>(checked_row(rows[i], nrows_s)) * lds_ + j];
     };
     int m;
     out[j] = keep == 0 ? __builtin_nan("")
-                       : bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return rank_slots[p * 32 + t]; },
+                       : bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return rank_slots[p * L + t]; },
                                               &m);
   }
 }
@@ -1071,22 +1078,31 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows
   SRA_HIP(hipMemsetAsync(nf_count, 0, sizeof(int), s));
   if (theta > kFinalMaxTheta) {
     const int pn = next_pow2(theta);
-    const size_t lds_bytes = sizeof(float) * static_cast<size_t>(pn) * 64;
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(bulyan_final_lds_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       static_cast<int>(sizeof(float) * kBigMaxClients * 64));
-    SRA_REQUIRE(attr == hipSuccess, SRA_ERR_UNSUPPORTED, "bulyan_final_lds_kernel: cannot reserve %zu bytes of LDS",
-                sizeof(float) * kBigMaxClients * 64);
-    hipLaunchKernelGGL(bulyan_final_lds_kernel, dim3(cdiv(d, 64)), dim3(256), lds_bytes, s, S, lds_, rows, nrows_s,
-                       theta, pn, keep, d, out, nf_count, nf_list);
-    int rc = launch_status("bulyan_final_lds_kernel");
+    constexpr int kStageLdsFloats = 512 * 64;   // 128 KiB: TW = kStageLdsFloats / pn coordinates per tile
+    const size_t lds_bytes = sizeof(float) * static_cast<size_t>(kStageLdsFloats);
+    int rc = SRA_OK;
+    auto run = [&](auto kern, int tw) -> int {
+      SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds_bytes)));
+      hipLaunchKernelGGL(kern, dim3(cdiv(d, tw)), dim3(256), sizeof(float) * static_cast<size_t>(pn) * tw, s, S, lds_,
+                         rows, nrows_s, theta, pn, keep, d, out, nf_count, nf_list);
+      return launch_status("bulyan_final_lds_kernel");
+    };
+    switch (kStageLdsFloats / pn) {
+      case 64: rc = run(bulyan_final_lds_kernel<64>, 64); break;
+      case 32: rc = run(bulyan_final_lds_kernel<32>, 32); break;
+      case 16: rc = run(bulyan_final_lds_kernel<16>, 16); break;
+      case 8: rc = run(bulyan_final_lds_kernel<8>, 8); break;
+      default: rc = run(bulyan_final_lds_kernel<4>, 4); break;
+    }
     if (rc) return rc;
-    static const hipError_t attr_l = hipFuncSetAttribute(reinterpret_cast<const void*>(bulyan_listed_big_kernel),
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                         static_cast<int>(sizeof(int) * kBigMaxClients * 32));
-    SRA_REQUIRE(attr_l == hipSuccess, SRA_ERR_UNSUPPORTED, "bulyan_listed_big_kernel: cannot reserve its LDS");
-    hipLaunchKernelGGL(bulyan_listed_big_kernel, dim3(256), dim3(32), sizeof(int) * static_cast<size_t>(theta) * 32, s,
-                       S, lds_, rows, nrows_s, theta, keep, nf_count, nf_list, out);
+    constexpr int kRankSlots = 1024 * 32;   // 128 KiB of rank slots
+    const int lanes = kRankSlots / theta < 32 ? kRankSlots / theta : 32;
+    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(bulyan_listed_big_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(sizeof(int) * kRankSlots)));
+    hipLaunchKernelGGL(bulyan_listed_big_kernel, dim3(256), dim3(lanes),
+                       sizeof(int) * static_cast<size_t>(theta) * lanes, s, S, lds_, rows, nrows_s, theta, keep,
+                       nf_count, nf_list, out);
     return launch_status("bulyan_listed_big_kernel");
   }
   int rc = SRA_ERR_UNSUPPORTED;
@@ -1130,9 +1146,17 @@ static int launch_round_big(const float* X, int64_t ldx, const int* rows, int nr
   if (nr <= 256)
     hipLaunchKernelGGL(dist_rows_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, rows, nrows_x, nr, d, agg, bpart,
                        static_cast<int>(blocks), static_cast<int>(tpb));
-  else
+  else if (nr <= 512)
     hipLaunchKernelGGL(dist_rows_kernel<2>, dim3(blocks), dim3(256), 0, s, X, ldx, rows, nrows_x, nr, d, agg, bpart,
                        static_cast<int>(blocks), static_cast<int>(tpb));
+  else   // groups of up to 1024 listed rows, each with its own slice of the partial table
+    for (int g0 = 0; g0 < nr; g0 += kDistRowGroup) {
+      const int ng = nr - g0 < kDistRowGroup ? nr - g0 : kDistRowGroup;
+      hipLaunchKernelGGL(dist_rows_kernel<4>, dim3(blocks), dim3(256), 0, s, X, ldx, rows + g0, nrows_x, ng, d, agg,
+                         bpart + static_cast<int64_t>(g0) * blocks, static_cast<int>(blocks), static_cast<int>(tpb));
+      const int rc2 = launch_status("dist_rows_kernel");
+      if (rc2) return rc2;
+    }
   return launch_status("dist_rows_kernel");
 }
 

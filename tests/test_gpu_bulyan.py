@@ -188,3 +188,40 @@ def test_stage_f32_many_rows(theta, beta):
         warnings.simplefilter("ignore")
         want = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j].astype(np.float64), beta) for j in range(d)])
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15, equal_nan=True)
+
+
+@pytest.mark.parametrize("mode,n,f", [("median", 600, 40), ("trimmedmean", 600, 40), ("median", 1100, 60),
+                                      ("trimmedmean", 1100, 60), ("krum", 600, 40)])
+def test_bulyan_beyond_512_clients(mode, n, f):
+    """No client ceiling the reference lacks (robust_estimator.py:277-332):
+    rounds with more than 512 remaining clients take the LDS k-select with
+    row groups of 1024 for the distances, Bulyan-Krum the N > 512 Krum rounds,
+    and theta = 520 / 980 the stage with a 32-coordinate LDS tile."""
+    x = make_rows(n, 120, seed=7 + n + f, byz=f)
+    want, _ = _leftfirst_and_ties(list(x), f, mode)
+    got = engine.bulyan(torch.from_numpy(x).cuda(), f, mode).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("theta,beta", [(600, 200), (1030, 900), (2100, 37)])
+def test_stage_f32_beyond_512_rows(theta, beta):
+    """The stage for theta > 512 (16- and 32-coordinate LDS tiles; the stage
+    by definition for NaN / inf / wide columns with fewer lanes per block)."""
+    rng = np.random.default_rng(theta + beta)
+    d = 70
+    S = (0.01 * rng.standard_normal((theta, d))).astype(np.float32)
+    S[:, 10:20] = rng.integers(-3, 4, size=(theta, 10)).astype(np.float32)
+    for c in range(20, 30):
+        r = rng.choice(theta, 2, replace=False)
+        S[r[0], c] *= 1e-12
+        S[r[1], c] *= 1e-30
+    S[rng.integers(0, theta), 30] = np.nan
+    S[rng.integers(0, theta), 31] = np.inf
+    S[:2, 32] = -np.inf
+    S[:, 33] = 0.0
+    got = engine.bulyan_stage(torch.from_numpy(S).cuda(), beta).cpu().numpy()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j].astype(np.float64), beta) for j in range(d)])
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15, equal_nan=True)
