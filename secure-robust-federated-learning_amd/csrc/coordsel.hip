@@ -618,7 +618,7 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
     return launch_status("select_quad_kernel");
   }
   const int pn = next_pow2(n);
-  SRA_REQUIRE(pn <= kLdsFloats / 4, SRA_ERR_UNSUPPORTED, "k-select supports N <= %d (got %d)", kLdsFloats / 4, n);
+  SRA_REQUIRE(pn <= kLdsFloats, SRA_ERR_UNSUPPORTED, "k-select supports N <= %d (got %d)", kLdsFloats, n);
   const int tile = kLdsFloats / pn;
   const int64_t lblocks = cdiv(d, tile);
   hipLaunchKernelGGL(select_lds_kernel, dim3(lblocks), dim3(256), sizeof(float) * pn * tile, s, X, n, pn, tile, d,

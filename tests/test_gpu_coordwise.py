@@ -35,7 +35,7 @@ def test_golden_coordwise(rec):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 7, 15, 16, 17, 31, 33, 64, 65, 99, 100, 101, 127, 128, 129, 200, 256, 512, 1000])
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 15, 16, 17, 31, 33, 64, 65, 99, 100, 101, 127, 128, 129, 200, 256, 512, 1000, 4097, 9000])   # > 4096: 1 coordinate per LDS tile
 def test_every_register_and_lds_bucket(n):
     d = 1031  # not a multiple of 4 / 256: exercises tail lanes
     x = make_rows(n, d, seed=1000 + n)
