@@ -238,8 +238,9 @@ int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes)
  * mode 1: robust_estimator.ex_noregret (src/robust_estimator.py:42-133).
  * The layer (n x d) is cut into itv-wide chunks (last one partial); each chunk
  * is filtered in client space from its centred fp64-MFMA Gram (top eigenpair
- * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 512 (n > 128: the
- * Gram in global memory, a 1024-thread re-orthogonalising solver per chunk).
+ * by Lanczos, fp64).  out: d float64 values.  1 <= n <= 1024 (n > 128: the
+ * Gram in global memory, a 1024-thread re-orthogonalising solver per chunk,
+ * two threads per client row up to n = 512, one above).
  * status: two device int32, zeroed by the caller.  ex_noregret whose
  * capped-simplex projection has no feasible candidate (projected_c = None,
  * robust_estimator.py:99) continues like the reference: the next iteration

@@ -589,11 +589,15 @@ __device__ __attribute__((noinline)) bool kl_project_t(double* ci_io, bool ai, i
   int stop = 1 << 30;
   if (tid < nk) {
     const int i = tid;
-    const double clip = 1.0 - np_pw64(0, i + 1, [&](int) { return cap; });
+    auto pw = [&](int lo, int cnt, auto&& g) -> double {
+      if constexpr (NP > 512) return np_pw64_rec<4>(lo, cnt, g);
+      else return np_pw64(lo, cnt, g);
+    };
+    const double clip = 1.0 - pw(0, i + 1, [&](int) { return cap; });
     if (clip <= 0.0) {
       stop = i;
     } else if (i + 1 < nk) {
-      const double norm = np_pw64(i + 1, nk - i - 1, [&](int q2) { return sv[q2]; });
+      const double norm = pw(i + 1, nk - i - 1, [&](int q2) { return sv[q2]; });
       scale = clip / norm;
       if (!(sv[i + 1] * scale > cap)) {
         double head = 0.0;
@@ -2186,6 +2190,7 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
 // filter (C5 filters 128 bucket means).
 // ============================================================================
 constexpr int NBIG = 512;
+constexpr int NBIG2 = 1024;        // N in (512, 1024]: one thread per row (filter_big_kernel<MODE, NBIG2>)
 constexpr int kBigThreads = 1024;
 constexpr int kBigWaves = kBigThreads / 64;
 constexpr int kBatchBig = 256;     // chunks per workspace batch
@@ -2308,12 +2313,13 @@ __device__ float np_pw32_big(int m, F&& f) {
   return half(0, m2) + half(m2, m - m2);
 }
 
+template <int NB>
 __global__ void __launch_bounds__(kBigThreads) noregret_pre_big_kernel(const double* __restrict__ Gb, int n, double eps,
                                                                        int* __restrict__ act, double* __restrict__ misc) {
-  __shared__ float srt[kBigWaves][NBIG];
-  __shared__ double diag[NBIG];
-  __shared__ double score[NBIG];
-  __shared__ int keep[NBIG];
+  __shared__ float srt[kBigWaves][NB];
+  __shared__ double diag[NB];
+  __shared__ double score[NB];
+  __shared__ int keep[NB];
   __shared__ float red[kBigWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x;
@@ -2349,14 +2355,17 @@ __global__ void __launch_bounds__(kBigThreads) noregret_pre_big_kernel(const dou
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
-    if (lane == 0) score[row] = static_cast<double>(np_pw32_big(m, [&](int q) { return sr[q]; }));
+    if (lane == 0) {
+      if constexpr (NB > NBIG) score[row] = static_cast<double>(np_pw32_rec<4>(0, m, [&](int q) { return sr[q]; }));
+      else score[row] = static_cast<double>(np_pw32_big(m, [&](int q) { return sr[q]; }));
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
   // argpartition(metric, -f)[:-f]: drop the fp largest (ties: the later index first)
-  if (tid < NBIG) {
+  if (tid < NB) {
     int kp = 0;
     if (tid < n) {
       const double si = score[tid];
@@ -2365,7 +2374,7 @@ __global__ void __launch_bounds__(kBigThreads) noregret_pre_big_kernel(const dou
       kp = above >= fp ? 1 : 0;
     }
     keep[tid] = kp;
-    act[static_cast<size_t>(b) * NBIG + tid] = kp;
+    act[static_cast<size_t>(b) * NB + tid] = kp;
   }
   __syncthreads();
   float md = 0.f;
@@ -2392,8 +2401,8 @@ __global__ void __launch_bounds__(kBigThreads) noregret_pre_big_kernel(const dou
 
 struct BigArgs {
   const double* G;   // [nb][n][n]
-  double* c;         // [nb][NBIG]
-  int* act;          // [nb][NBIG]
+  double* c;         // [nb][NB]
+  int* act;          // [nb][NB]
   double* misc;      // [nb][kMisc]
   int* status;
   int n;
@@ -2401,37 +2410,43 @@ struct BigArgs {
   double eps;
   double sigma;
   double expansion;
-  double* Vg;        // [grid][LMAX][NBIG]
+  double* Vg;        // [grid][LMAX][NB]
   int* trace;        // optional [nb][1 + 2 n] decision trace (batch-relative), the small path's layout
 };
 
 constexpr int kHStride = LMAX + 2;
-constexpr size_t kBigLds =
-    sizeof(double) * (4 * NBIG + kBigWaves * kHStride + kHStride + 2 * 4 * kBigWaves + kBigWaves * TRI + 4 * NBIG) +
-    sizeof(int) * (3 * NBIG + 4 * kBigWaves + 16);
-static_assert(kBigLds <= 163840, "the big solver's LDS must fit one CU");
+constexpr size_t big_lds(int nb) {
+  return sizeof(double) * (4 * nb + kBigWaves * kHStride + kHStride + 2 * 4 * kBigWaves + kBigWaves * TRI + 4 * nb) +
+         sizeof(int) * (3 * nb + 4 * kBigWaves + 16);
+}
+constexpr size_t kBigLds = big_lds(NBIG);
+static_assert(big_lds(NBIG2) <= 163840, "the big solver's LDS must fit one CU");
 
-template <int MODE>
+// NB = NBIG: 1024 threads = two per row (the two column halves of every
+// matvec); NB = NBIG2: one thread per row, the matvec over all columns.
+template <int MODE, int NB = NBIG>
 __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
+  constexpr int HALVES = kBigThreads / NB;
+  static_assert(HALVES == 1 || HALVES == 2, "one or two threads per row");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* xbuf = reinterpret_cast<double*>(smem);   // [NBIG] operator input
-  double* ysum = xbuf + NBIG;                       // [2][NBIG] matvec halves
-  double* rbuf = ysum + 2 * NBIG;                   // [NBIG] scratch
-  double* hpart = rbuf + NBIG;                      // [kBigWaves][kHStride] per-wave dot products
+  double* xbuf = reinterpret_cast<double*>(smem);   // [NB] operator input
+  double* ysum = xbuf + NB;                         // [2][NB] matvec halves
+  double* rbuf = ysum + 2 * NB;                     // [NB] scratch
+  double* hpart = rbuf + NB;                        // [kBigWaves][kHStride] per-wave dot products
   double* hbuf = hpart + kBigWaves * kHStride;      // [kHStride] Gram-Schmidt coefficients (+ |r''|^2)
   double* red = hbuf + kHStride;                    // [2][4 kBigWaves] block reductions
   double* tri = red + 2 * 4 * kBigWaves;            // [kBigWaves][TRI] per-wave tridiagonal record
-  double* cvec = tri + kBigWaves * TRI;             // [NBIG]
-  double* vscr = cvec + NBIG;                       // [3][NBIG]
-  int* ibuf = reinterpret_cast<int*>(vscr + 3 * NBIG);   // [3][NBIG] + [4][kBigWaves] + [16]
+  double* cvec = tri + kBigWaves * TRI;             // [NB]
+  double* vscr = cvec + NB;                         // [3][NB]
+  int* ibuf = reinterpret_cast<int*>(vscr + 3 * NB);   // [3][NB] + [4][kBigWaves] + [16]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row = tid & (NBIG - 1);
-  const int half = tid >> 9;       // which half of every matvec's columns
-  const bool own = half == 0;      // the first 512 threads speak for their row
+  const int row = tid & (NB - 1);
+  const int half = tid / NB;       // which half of every matvec's columns (HALVES == 2)
+  const bool own = half == 0;      // the first NB threads speak for their row
   const int n = A.n;
   double* trw = tri + wave * TRI;
-  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * LMAX * NBIG;
+  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * LMAX * NB;
 
   int rslot = 0;
   auto reduce4 = [&](double v0, double v1, double v2, double v3, double (&o)[4], int nv) {
@@ -2465,7 +2480,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
       }
     }
     double* R = red + 4 * kBigWaves * rslot;
-    int* I = ibuf + 3 * NBIG + 2 * kBigWaves * rslot;
+    int* I = ibuf + 3 * NB + 2 * kBigWaves * rslot;
     if (lane == 0) {
       R[wave] = v;
       I[wave] = i;
@@ -2485,7 +2500,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
   // y_row = sum_j G[j][row] x_j (G symmetric): each half sums its columns in
   // order, the halves are added in a fixed order
   auto gmv = [&](const double* G) -> double {
-    const int hn = (n + 1) >> 1;
+    const int hn = (n + HALVES - 1) / HALVES;
     const int j0 = half * hn, j1 = j0 + hn < n ? j0 + hn : n;
     double p0 = 0.0, p1 = 0.0;
     if (row < n) {
@@ -2497,15 +2512,20 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
       if (j < j1) p0 = fma(G[static_cast<size_t>(j) * n + row], xbuf[j], p0);
     }
     // ysum is rewritten by the next gmv only after a reduction's barrier
-    ysum[half * NBIG + row] = p0 + p1;
-    __syncthreads();
-    return ysum[row] + ysum[NBIG + row];
+    if constexpr (HALVES == 1) {
+      __syncthreads();   // every thread has read xbuf before it is rewritten
+      return p0 + p1;
+    } else {
+      ysum[half * NB + row] = p0 + p1;
+      __syncthreads();
+      return ysum[row] + ysum[NB + row];
+    }
   };
 
   for (int ch = blockIdx.x; ch < A.nb; ch += gridDim.x) {
     const double* G = A.G + static_cast<size_t>(ch) * n * n;
     bool ai;
-    if constexpr (MODE == 1) ai = own && row < n && A.act[static_cast<size_t>(ch) * NBIG + row] != 0;
+    if constexpr (MODE == 1) ai = own && row < n && A.act[static_cast<size_t>(ch) * NB + row] != 0;
     else ai = own && row < n;
     double ci = ai ? 1.0 : 0.0;
     const int fdrop = static_cast<int>(ceil(A.eps * n));
@@ -2588,7 +2608,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
           const double cx = y - gwi * S1 - GY + sgw * S1;
           const double ib = 1.0 / bet;
           const double q = rt * ib;
-          if (own && row < n) Vb[static_cast<size_t>(j) * NBIG + row] = q;
+          if (own && row < n) Vb[static_cast<size_t>(j) * NB + row] = q;
           const double rp = swi * cx * ib - (j > 0 ? bet * qprev : 0.0);
           qprev = q;
           reduce4(own ? swi * rt * y : 0.0, 0.0, 0.0, 0.0, o, 1);
@@ -2601,7 +2621,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
             const int nh = pass == 0 ? j + 2 : j + 1;
             for (int qq = 0; qq < nh; ++qq) {
               double v = 0.0;
-              if (own && row < n) v = qq <= j ? Vb[static_cast<size_t>(qq) * NBIG + row] * r : r * r;
+              if (own && row < n) v = qq <= j ? Vb[static_cast<size_t>(qq) * NB + row] * r : r * r;
               v = wave_sum(v);
               if (lane == 0) hpart[wave * kHStride + qq] = v;
             }
@@ -2616,7 +2636,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
             double upd = 0.0, hn2 = 0.0;
             for (int qq = 0; qq <= j; ++qq) {
               const double hv = hbuf[qq];
-              if (own && row < n) upd = fma(hv, Vb[static_cast<size_t>(qq) * NBIG + row], upd);
+              if (own && row < n) upd = fma(hv, Vb[static_cast<size_t>(qq) * NB + row], upd);
               hn2 = fma(hv, hv, hn2);
             }
             r -= upd;
@@ -2640,7 +2660,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
           const int m = converged ? m_conv : LMAX;
           double u0 = 0.0;
           if (own && row < n)
-            for (int qq = 0; qq < m; ++qq) u0 = fma(trw[128 + qq], Vb[static_cast<size_t>(qq) * NBIG + row], u0);
+            for (int qq = 0; qq < m; ++qq) u0 = fma(trw[128 + qq], Vb[static_cast<size_t>(qq) * NB + row], u0);
           ui = u0;
         }
         if (converged || restarts == kMaxRestarts) break;
@@ -2678,7 +2698,7 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
         const double cap = 1.0 / (1.0 - A.eps) / nk;
         if (ai) ci = ci * (1.0 - step * ti);
         int capped = 0;
-        if (!kl_project_t<NBIG, kBigWaves>(&ci, ai, row, own && row < n, nk, cap, cvec, vscr, ibuf, red, hbuf,
+        if (!kl_project_t<NB, kBigWaves>(&ci, ai, row, own && row < n, nk, cap, cvec, vscr, ibuf, red, hbuf,
                                             &capped)) {
           none = true;   // projected_c = None (:99)
           unweighted = it + 1 == iters;
@@ -2695,17 +2715,19 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
     __syncthreads();
     if (own) {
       cvec[row] = ai ? ci : 0.0;
-      ibuf[2 * NBIG + row] = ai ? 1 : 0;
-      A.c[static_cast<size_t>(ch) * NBIG + row] = ai ? ci : 0.0;
-      A.act[static_cast<size_t>(ch) * NBIG + row] = ai ? 1 : 0;
+      ibuf[2 * NB + row] = ai ? 1 : 0;
+      A.c[static_cast<size_t>(ch) * NB + row] = ai ? ci : 0.0;
+      A.act[static_cast<size_t>(ch) * NB + row] = ai ? 1 : 0;
     }
     __syncthreads();
     if (tid == 0) {
       int q2 = 0;
       double* kept = vscr;
       for (int i = 0; i < n; ++i)
-        if (ibuf[2 * NBIG + i]) kept[q2++] = cvec[i];
-      A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int z) { return kept[z]; });
+        if (ibuf[2 * NB + i]) kept[q2++] = cvec[i];
+      auto kz = [&](int z) { return kept[z]; };
+      if constexpr (NB > NBIG) A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64_rec<4>(0, q2, kz);
+      else A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, kz);
       A.misc[static_cast<size_t>(ch) * kMisc + 2] = unweighted ? 1.0 : 0.0;
       if (unweighted) atomicAdd(A.status + 1, 1);
     }
@@ -2720,14 +2742,16 @@ __global__ void __launch_bounds__(kBigThreads) filter_big_kernel(BigArgs A) {
 constexpr size_t kChunkWsBytes = sizeof(double) * (FNP * FNP + FNP + kMisc) + sizeof(int) * (FNP + 1);
 constexpr int kLanczosGrid = 512;    // workgroups of lanczos_solve_kernel: 2 per CU, each owns a basis slot
 
-// N > FNP: [G nb n n][c nb NBIG][misc nb kMisc][mu nb itv][V grid LMAX NBIG][act nb NBIG]
+// N > FNP: [G nb n n][c nb NB][misc nb kMisc][mu nb itv][V grid LMAX NB][act nb NB], NB = NBIG or NBIG2
+static int big_rows(int n) { return n > NBIG ? NBIG2 : NBIG; }
 static size_t filter_big_workspace_bytes(int n, int64_t d, int itv) {
   const int64_t nchunks = cdiv(d, itv);
   const int64_t b = nchunks < kBatchBig ? nchunks : kBatchBig;
   const int64_t grid = b < kBigGrid ? b : kBigGrid;
-  return 256 + static_cast<size_t>(b) * (sizeof(double) * (static_cast<size_t>(n) * n + NBIG + kMisc + itv) +
-                                         sizeof(int) * NBIG) +
-         static_cast<size_t>(grid) * LMAX * NBIG * sizeof(double) + 256;
+  const size_t NB = big_rows(n);
+  return 256 + static_cast<size_t>(b) * (sizeof(double) * (static_cast<size_t>(n) * n + NB + kMisc + itv) +
+                                         sizeof(int) * NB) +
+         static_cast<size_t>(grid) * LMAX * NB * sizeof(double) + 256;
 }
 
 int launch_filter_big(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
@@ -2735,21 +2759,30 @@ int launch_filter_big(int mode, const float* X, int n, int64_t d, int64_t ldx, i
   const int64_t nchunks = cdiv(d, itv);
   const int64_t bmax = nchunks < kBatchBig ? nchunks : kBatchBig;
   const int grid_max = static_cast<int>(bmax < kBigGrid ? bmax : kBigGrid);
+  const int NB = big_rows(n);
+  const bool wide = NB == NBIG2;
+  const size_t lds = wide ? big_lds(NBIG2) : kBigLds;
   char* base = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
   double* Gws = reinterpret_cast<double*>(base);
   double* cws = Gws + static_cast<size_t>(bmax) * n * n;
-  double* mws = cws + static_cast<size_t>(bmax) * NBIG;
+  double* mws = cws + static_cast<size_t>(bmax) * NB;
   double* muws = mws + static_cast<size_t>(bmax) * kMisc;
   double* Vws = muws + static_cast<size_t>(bmax) * itv;
-  int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(grid_max) * LMAX * NBIG);
+  int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(grid_max) * LMAX * NB);
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&filter_big_kernel<0>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      static_cast<int>(kBigLds));
   static const hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&filter_big_kernel<1>),
                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                                       static_cast<int>(kBigLds));
-  SRA_REQUIRE(attr == hipSuccess && attr1 == hipSuccess, SRA_ERR_UNSUPPORTED,
-              "filter_big_kernel: cannot reserve %zu bytes of LDS", kBigLds);
+  static const hipError_t attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&filter_big_kernel<0, NBIG2>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      static_cast<int>(big_lds(NBIG2)));
+  static const hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&filter_big_kernel<1, NBIG2>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      static_cast<int>(big_lds(NBIG2)));
+  SRA_REQUIRE(attr == hipSuccess && attr1 == hipSuccess && attr2 == hipSuccess && attr3 == hipSuccess,
+              SRA_ERR_UNSUPPORTED, "filter_big_kernel: cannot reserve %zu bytes of LDS", lds);
   const int nbk = static_cast<int>(cdiv(n, kBigTile));
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
@@ -2763,19 +2796,27 @@ int launch_filter_big(int mode, const float* X, int n, int64_t d, int64_t ldx, i
     rc = launch_status("chunk_gram_big_kernel");
     if (rc) return rc;
     if (mode == 1) {
-      hipLaunchKernelGGL(noregret_pre_big_kernel, dim3(nb), dim3(kBigThreads), 0, s, Gws, n, eps, aws, mws);
+      if (wide)
+        hipLaunchKernelGGL(noregret_pre_big_kernel<NBIG2>, dim3(nb), dim3(kBigThreads), 0, s, Gws, n, eps, aws, mws);
+      else
+        hipLaunchKernelGGL(noregret_pre_big_kernel<NBIG>, dim3(nb), dim3(kBigThreads), 0, s, Gws, n, eps, aws, mws);
       rc = launch_status("noregret_pre_big_kernel");
       if (rc) return rc;
     }
     BigArgs ba{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, Vws,
                trace != nullptr ? trace + static_cast<size_t>(c0) * (1 + 2 * n) : nullptr};
     const int grid = nb < grid_max ? nb : grid_max;
-    if (mode == 0) hipLaunchKernelGGL(filter_big_kernel<0>, dim3(grid), dim3(kBigThreads), kBigLds, s, ba);
-    else hipLaunchKernelGGL(filter_big_kernel<1>, dim3(grid), dim3(kBigThreads), kBigLds, s, ba);
+    if (wide) {
+      if (mode == 0) hipLaunchKernelGGL((filter_big_kernel<0, NBIG2>), dim3(grid), dim3(kBigThreads), lds, s, ba);
+      else hipLaunchKernelGGL((filter_big_kernel<1, NBIG2>), dim3(grid), dim3(kBigThreads), lds, s, ba);
+    } else {
+      if (mode == 0) hipLaunchKernelGGL(filter_big_kernel<0>, dim3(grid), dim3(kBigThreads), kBigLds, s, ba);
+      else hipLaunchKernelGGL(filter_big_kernel<1>, dim3(grid), dim3(kBigThreads), kBigLds, s, ba);
+    }
     rc = launch_status("filter_big_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws, aws,
-                       mws, out, NBIG, mode);
+                       mws, out, NB, mode);
     rc = launch_status("chunk_mean_kernel");
     if (rc) return rc;
   }
@@ -2793,7 +2834,7 @@ size_t filter_workspace_bytes(int n, int64_t d, int itv) {
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
                   double expansion, double* out, int* status, double* dbg, int* trace, void* ws, size_t ws_bytes,
                   hipStream_t s) {
-  SRA_REQUIRE(n >= 1 && n <= NBIG, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", NBIG, n);
+  SRA_REQUIRE(n >= 1 && n <= NBIG2, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", NBIG2, n);
   SRA_REQUIRE(itv >= 1, SRA_ERR_ARG, "itv must be >= 1");
   const int64_t nchunks = cdiv(d, itv);
   SRA_REQUIRE(nchunks < (int64_t(1) << 31), SRA_ERR_ARG, "too many chunks");

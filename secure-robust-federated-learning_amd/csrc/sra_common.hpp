@@ -542,4 +542,51 @@ __device__ __forceinline__ double np_pw64(int lo, int n, F&& f) {
   return half(lo, n2) + half(lo + n2, n - n2);
 }
 
+// numpy's pairwise sum at any split depth (fp64 / fp32): DEPTH levels of the
+// split at n/2 rounded down to a multiple of 8 cover n <= 128 * 2^DEPTH - 16.
+// Used by the N > 512 paths; np_pw64 above stays the <= 512 form.
+template <int DEPTH, typename F>
+__device__ __forceinline__ double np_pw64_rec(int lo, int n, F&& f) {
+  if constexpr (DEPTH == 0) {
+    return np_pw_block64(n, [&](int i) { return f(lo + i); });
+  } else {
+    if (n <= 128) return np_pw_block64(n, [&](int i) { return f(lo + i); });
+    int q = n / 2;
+    q -= q % 8;
+    const double a = np_pw64_rec<DEPTH - 1>(lo, q, f);
+    return a + np_pw64_rec<DEPTH - 1>(lo + q, n - q, f);
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ float np_pw_block32(int n, F&& f) {
+  if (n < 8) {
+    float res = 0.f;
+    for (int i = 0; i < n; ++i) res += f(i);
+    return res;
+  }
+  float r0 = f(0), r1 = f(1), r2 = f(2), r3 = f(3), r4 = f(4), r5 = f(5), r6 = f(6), r7 = f(7);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += f(i); r1 += f(i + 1); r2 += f(i + 2); r3 += f(i + 3);
+    r4 += f(i + 4); r5 += f(i + 5); r6 += f(i + 6); r7 += f(i + 7);
+  }
+  float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += f(i);
+  return res;
+}
+
+template <int DEPTH, typename F>
+__device__ __forceinline__ float np_pw32_rec(int lo, int n, F&& f) {
+  if constexpr (DEPTH == 0) {
+    return np_pw_block32(n, [&](int i) { return f(lo + i); });
+  } else {
+    if (n <= 128) return np_pw_block32(n, [&](int i) { return f(lo + i); });
+    int q = n / 2;
+    q -= q % 8;
+    const float a = np_pw32_rec<DEPTH - 1>(lo, q, f);
+    return a + np_pw32_rec<DEPTH - 1>(lo + q, n - q, f);
+  }
+}
+
 }  // namespace sra

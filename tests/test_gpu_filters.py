@@ -240,12 +240,13 @@ def test_c5_mom_filterl2_per_gpu_shard_chunks():
 
 
 @pytest.mark.parametrize("n,k,itv,eps", [(129, 300, 150, 0.03), (200, 300, 150, 0.02), (256, 256, 256, 0.02),
-                                         (512, 300, 300, 0.01)])
+                                         (512, 300, 300, 0.01), (700, 300, 300, 0.005), (1024, 256, 256, 0.004)])
 def test_filterl2_many_clients(n, k, itv, eps):
     """N > 128 (the reference has no client limit): the big-N path (global
-    Gram blocks, the 1024-thread re-orthogonalising solver) against the
-    oracle over a few iterations (sigma 1e-5: no early exit), including
-    N > itv (client space larger than the chunk)."""
+    Gram blocks, the 1024-thread re-orthogonalising solver: two threads per
+    row up to N = 512, one above) against the oracle over a few iterations
+    (sigma 1e-5: no early exit), including N > itv (client space larger than
+    the chunk)."""
     x = make_rows(n, k, seed=700 + n, byz=max(1, n // 6))
     want = orc.filterL2(list(x), eps, 1e-5, 20, itv)
     got = engine.filter_l2(torch.from_numpy(x).cuda(), eps, 1e-5, 20, itv).cpu().numpy()
@@ -253,7 +254,7 @@ def test_filterl2_many_clients(n, k, itv, eps):
 
 
 @pytest.mark.parametrize("n,k,itv,eps", [(129, 200, 100, 0.05), (200, 200, 200, 0.03), (256, 150, 150, 0.03),
-                                         (512, 128, 128, 0.01)])
+                                         (512, 128, 128, 0.01), (700, 128, 128, 0.005), (1024, 100, 100, 0.004)])
 def test_ex_noregret_many_clients(n, k, itv, eps):
     x = make_rows(n, k, seed=800 + n, byz=max(1, n // 6))
     with warnings.catch_warnings():
@@ -263,7 +264,8 @@ def test_ex_noregret_many_clients(n, k, itv, eps):
     np.testing.assert_allclose(got, want, rtol=2e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize("mode,n,k,eps", [(0, 200, 400, 0.1), (0, 512, 300, 0.05), (1, 256, 300, 0.05)])
+@pytest.mark.parametrize("mode,n,k,eps", [(0, 200, 400, 0.1), (0, 512, 300, 0.05), (1, 256, 300, 0.05),
+                                          (0, 1000, 300, 0.01), (1, 800, 200, 0.01)])
 def test_many_clients_decision_trace(mode, n, k, eps):
     """Long runs at N > 128 (sigma 1e-5): the device's per-iteration decisions
     (removed client / capped count, the final active set) equal the
