@@ -220,7 +220,7 @@ int sra_bulyan_stage_f32(const float* S, int64_t theta, int64_t d, int64_t lds, 
  * (optional) = np.argmin of the pairwise-summed distance rows (first NaN if
  * any); median_row (optional, theta x d, row stride ldr) = that distance row;
  * out[j] = mean of arr[argsort(row)[:beta]] (Python slice semantics; equal
- * distances take the smaller value first).  1 <= theta <= 512. */
+ * distances take the smaller value first).  1 <= theta <= 8192. */
 int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t d, int64_t lda, int32_t beta, double* out,
                               int64_t* median_index, double* median_row, int64_t ldr, void* stream);
 

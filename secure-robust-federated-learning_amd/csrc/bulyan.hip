@@ -1004,20 +1004,24 @@ inline int bulyan_keep(int theta, int beta) {
   return theta + beta > 0 ? theta + beta : 0;
 }
 
-// the drop-in's scalar helpers: one lane per column of a float64 theta x d matrix
-constexpr int kCoordMaxTheta = 512;
+// the drop-in's scalar helpers: one lane per column of a float64 theta x d
+// matrix; the rank slots [theta][L] in dynamic LDS, L = min(64, 32768 / theta)
+// lanes per block (128 KiB at most)
+constexpr int kCoordMaxTheta = kBigMaxClients;
+constexpr int kCoordSlots = 512 * 64;
 
 __global__ void __launch_bounds__(64) bulyan_coord_f64_kernel(const double* __restrict__ A, int theta, int64_t d,
                                                               int64_t lda, int keep, double* __restrict__ out,
                                                               int64_t* __restrict__ midx, double* __restrict__ mrow,
                                                               int64_t ldr) {
-  __shared__ int order[kCoordMaxTheta][64];
+  extern __shared__ int order_slots[];   // [theta][blockDim.x]
   const int t = threadIdx.x;
-  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + t;
+  const int L = blockDim.x;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * L + t;
   if (j >= d) return;
   auto a = [&](int i) -> double { return A[static_cast<int64_t>(i) * lda + j]; };
   int m;
-  out[j] = bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return order[p][t]; }, &m);
+  out[j] = bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return order_slots[p * L + t]; }, &m);
   if (midx) midx[j] = m;
   if (mrow) {
     const double am = a(m);
@@ -1295,7 +1299,13 @@ extern "C" int sra_bulyan_coordinate_f64(const double* A, int64_t theta, int64_t
               kCoordMaxTheta, static_cast<long long>(theta));
   SRA_REQUIRE(d >= 1 && lda >= d && (median_row == nullptr || ldr >= d), SRA_ERR_SHAPE, "bad d / lda / ldr");
   const int keep = bulyan_keep(static_cast<int>(theta), beta);
-  hipLaunchKernelGGL(bulyan_coord_f64_kernel, dim3(cdiv(d, 64)), dim3(64), 0, static_cast<hipStream_t>(stream), A,
+  const int lanes = kCoordSlots / theta < 64 ? static_cast<int>(kCoordSlots / theta) : 64;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(bulyan_coord_f64_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     static_cast<int>(sizeof(int) * kCoordSlots));
+  SRA_REQUIRE(attr == hipSuccess, SRA_ERR_UNSUPPORTED, "bulyan_coord_f64_kernel: cannot reserve its LDS");
+  hipLaunchKernelGGL(bulyan_coord_f64_kernel, dim3(cdiv(d, lanes)), dim3(lanes),
+                     sizeof(int) * static_cast<size_t>(theta) * lanes, static_cast<hipStream_t>(stream), A,
                      static_cast<int>(theta), d, lda, keep, out, median_index, median_row, ldr);
   return launch_status("bulyan_coord_f64_kernel");
 }

@@ -225,3 +225,21 @@ def test_stage_f32_beyond_512_rows(theta, beta):
         warnings.simplefilter("ignore")
         want = np.array([orc.bulyan_one_coordinate_leftfirst(S[:, j].astype(np.float64), beta) for j in range(d)])
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15, equal_nan=True)
+
+
+@pytest.mark.parametrize("theta,beta", [(700, 300), (2000, 1500)])
+def test_scalar_helpers_beyond_512(theta, beta):
+    """The drop-in's bulyan_median / bulyan_one_coordinate (robust_estimator.py:
+    259-275) on arrays longer than 512 (rank slots in dynamic LDS, fewer lanes
+    per block), against the oracle's restatement."""
+    import warnings
+    a = np.random.default_rng(theta).standard_normal(theta)
+    m, row = gre.bulyan_median(a)
+    wm, wrow = orc.bulyan_median(a)
+    assert int(m) == int(wm)
+    np.testing.assert_array_equal(row, wrow)
+    got = gre.bulyan_one_coordinate(a, beta)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want = orc.bulyan_one_coordinate_leftfirst(a, beta)
+    np.testing.assert_allclose(got, want, rtol=1e-15, atol=0)
