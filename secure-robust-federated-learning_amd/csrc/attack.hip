@@ -28,7 +28,7 @@ namespace sra {
 
 constexpr int kAtkBS = 256;
 constexpr int kAtkTile = 4096;        // columns per fp64 partial (sa_norms)
-constexpr int kAtkMaxClients = 256;   // as Krum
+constexpr int kAtkMaxClients = 2048;   // distance lists in LDS: 3 x 16 KiB fp64 + 8 KiB fp32
 
 size_t gram_workspace_bytes(int n, int64_t d);
 int launch_gram(const float* X, int n, int64_t d, int64_t ldx, double* G, void* ws, size_t ws_bytes, hipStream_t s);
@@ -207,7 +207,9 @@ __global__ void __launch_bounds__(kAtkBS) attack_krum_search_kernel(const float*
   }
   const int size_ = slice_len(m - 1 - 2, m - 1);
   // a malicious row: (c-1) exact zeros, then the sorted benign distances
-  if (tid == 0) smal = np_pw64(0, size_, [&](int q) { return q < c - 1 ? 0.0 : ds[q - (c - 1)]; });
+  // numpy's pairwise fp64 sum; lists above 512 need the deeper split
+  auto pw = [&](int cnt, auto&& g) -> double { return cnt <= 512 ? np_pw64(0, cnt, g) : np_pw64_rec<5>(0, cnt, g); };
+  if (tid == 0) smal = pw(size_, [&](int q) { return q < c - 1 ? 0.0 : ds[q - (c - 1)]; });
   // a benign row: its sorted benign list merged with c copies of dm[i] (any
   // split point inside a run of equal values yields the same sequence)
   for (int i = tid; i < nrows; i += kAtkBS) {
@@ -220,7 +222,7 @@ __global__ void __launch_bounds__(kAtkBS) attack_krum_search_kernel(const float*
       else hi = mid;
     }
     const int p = lo;
-    score[i] = np_pw64(0, size_, [&](int q) {
+    score[i] = pw(size_, [&](int q) {
       return q < p ? static_cast<double>(sb[q]) : (q < p + c ? dmi : static_cast<double>(sb[q - c]));
     });
   }

@@ -192,3 +192,20 @@ def test_attack_errors_match_reference_classes():
     grads, params = case_clients(CASES[3])
     with pytest.raises(ValueError):
         attack.attack_trimmedmean(_Net(params), grads, list(range(CASES[3]["m"])))
+
+
+def test_attack_krum_many_clients_vs_oracle():
+    """m = 600 clients (distance lists longer than 512: numpy's pairwise sum one
+    split level deeper), lambda and the malicious row against the oracle."""
+    from srfl_amd import attack
+    from synth import make_rows
+    m, d = 600, 48
+    x = make_rows(m, d, 4343)
+    mal = list(range(0, m, 7))
+    lam_ref, row_ref = orc.attack_krum([[x[c].copy()] for c in range(m)], mal, 0, 1e-8)
+    X = torch.from_numpy(x).cuda()
+    mask = torch.tensor([1 if c in mal else 0 for c in range(m)], dtype=torch.int32, device="cuda")
+    benign = torch.tensor([c for c in range(m) if c not in mal], dtype=torch.int32, device="cuda")
+    row, lam, pick = attack.attack_krum_layer(X, mask, benign, 1e-8)
+    assert float(lam.item()) == lam_ref
+    np.testing.assert_array_equal(row.cpu().numpy(), row_ref)
