@@ -462,13 +462,34 @@ __global__ void __launch_bounds__(256) dist_rows_kernel(const float* __restrict_
 // infinities are at NaN distance -> m = the first of them).  `slot(p)` is
 // per-lane scratch for the rank -> value-index map.
 // ---------------------------------------------------------------------------
-template <typename A, typename Slot>
+// DEEP: theta may exceed 512 (the N > 512 stage and the scalar helpers), so
+// the pairwise sums take numpy's split to seven levels there (exact to 16368).
+template <int DEPTH, typename F>
+__device__ __attribute__((noinline)) double np_pw64_deep(int lo, int n, F f) {
+  if constexpr (DEPTH == 0) {
+    return np_pw_block64(n, [&](int i) { return f(lo + i); });
+  } else {
+    if (n <= 128) return np_pw_block64(n, [&](int i) { return f(lo + i); });
+    int q = n / 2;
+    q -= q % 8;
+    const double l = np_pw64_deep<DEPTH - 1>(lo, q, f);
+    return l + np_pw64_deep<DEPTH - 1>(lo + q, n - q, f);
+  }
+}
+
+template <bool DEEP = false, typename A, typename Slot>
 __device__ double bulyan_stage_generic(A&& a, int theta, int keep, Slot&& slot, int* m_out) {
+  auto pw = [&](int n, auto&& g) -> double {
+    if constexpr (DEEP) {
+      if (n > 512) return np_pw64_deep<7>(0, n, g);
+    }
+    return np_pw64(0, n, g);
+  };
   int m = 0;
   double best = 0.0;
   for (int i = 0; i < theta; ++i) {
     const double ai = a(i);
-    const double T = np_pw64(0, theta, [&](int k) { return k == i ? 0.0 : __builtin_fabs(ai - a(k)); });
+    const double T = pw(theta, [&](int k) { return k == i ? 0.0 : __builtin_fabs(ai - a(k)); });
     if (__builtin_isnan(T)) {
       m = i;
       break;
@@ -498,7 +519,7 @@ __device__ double bulyan_stage_generic(A&& a, int theta, int keep, Slot&& slot, 
     slot(r) = k;
   }
   if (keep <= 0) return __builtin_nan("");
-  return np_pw64(0, keep, [&](int p) { return a(slot(p)); }) / static_cast<double>(keep);
+  return pw(keep, [&](int p) { return a(slot(p)); }) / static_cast<double>(keep);
 }
 
 // numpy's pairwise fp64 sum (np_pw_block64) of f(0..n) for n in (P - 16, P],
@@ -991,7 +1012,7 @@ __global__ void __launch_bounds__(32) bulyan_listed_big_kernel(const float* __re
     };
     int m;
     out[j] = keep == 0 ? __builtin_nan("")
-                       : bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return rank_slots[p * L + t]; },
+                       : bulyan_stage_generic<true>(a, theta, keep, [&](int p) -> int& { return rank_slots[p * L + t]; },
                                               &m);
   }
 }
@@ -1021,7 +1042,7 @@ __global__ void __launch_bounds__(64) bulyan_coord_f64_kernel(const double* __re
   if (j >= d) return;
   auto a = [&](int i) -> double { return A[static_cast<int64_t>(i) * lda + j]; };
   int m;
-  out[j] = bulyan_stage_generic(a, theta, keep, [&](int p) -> int& { return order_slots[p * L + t]; }, &m);
+  out[j] = bulyan_stage_generic<true>(a, theta, keep, [&](int p) -> int& { return order_slots[p * L + t]; }, &m);
   if (midx) midx[j] = m;
   if (mrow) {
     const double am = a(m);
