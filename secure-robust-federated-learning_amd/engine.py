@@ -170,9 +170,13 @@ MOM_KRUM_FUSED_MAX_BUCKETS = 192
 
 def gram_buckets(X, bucket_size=3):
     """Centred Gram (B x B float64) of the means of consecutive buckets of
-    clients, B = ceil(N / bucket_size) <= 192, without writing the means."""
+    clients, B = ceil(N / bucket_size): without writing the means up to 192
+    buckets of at most 4 clients (sra_gram_buckets_f32), else the Gram of the
+    materialised means (sra_bucket_mean_f32 + sra_gram_f32, B <= 8192)."""
     X, n, d, ldx = as_matrix(X)
     nb = -(-n // bucket_size)
+    if not (1 <= bucket_size <= 4 and nb <= MOM_KRUM_FUSED_MAX_BUCKETS):
+        return gram(bucket_means(X, bucket_size, nb))
     G = torch.empty((nb, nb), dtype=torch.float64, device=X.device)
     nbytes = _lib.query_bytes("sra_gram_workspace_bytes", nb, d)
     ws = _workspace(nbytes, X.device)

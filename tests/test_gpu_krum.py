@@ -207,3 +207,23 @@ def test_gram_beyond_512_clients():
     d2 = np.maximum(np.diag(gc)[:, None] + np.diag(gc)[None, :] - 2 * gc, 0.0)
     got = np.diag(G)[:, None] + np.diag(G)[None, :] - 2 * G
     np.testing.assert_allclose(got, d2, rtol=2e-5, atol=1e-9 * d2.max())
+
+
+def test_gram_buckets_beyond_fused_range():
+    """More than 192 buckets (a sharded mom_krum at N = 900): the bucket Gram
+    falls back to the Gram of the materialised means; its distances match an
+    fp64 evaluation of the means' distances, and sharded-style Krum over it
+    picks the oracle's bucket."""
+    n, d, f = 900, 3000, 20
+    x = make_rows(n, d, seed=515, byz=30)
+    X = torch.from_numpy(x).cuda()
+    G = engine.gram_buckets(X, 3).cpu().numpy()
+    B = np.array(orc.bucket_means(list(x), 3, 300), dtype=np.float64)
+    Bc = B - B.mean(axis=0)
+    gc = Bc @ Bc.T
+    d2 = np.maximum(np.diag(gc)[:, None] + np.diag(gc)[None, :] - 2 * gc, 0.0)
+    got = np.diag(G)[:, None] + np.diag(G)[None, :] - 2 * G
+    np.testing.assert_allclose(got, d2, rtol=2e-5, atol=1e-9 * d2.max())
+    order, _ = engine.krum_from_gram(torch.from_numpy(G).cuda(), f, 1, scores=False)
+    want = int(np.argmin(orc.krum_(list(B.astype(np.float32)), f)))
+    assert int(order.cpu()[0]) == want
