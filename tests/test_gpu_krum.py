@@ -223,7 +223,10 @@ def test_gram_buckets_beyond_fused_range():
     gc = Bc @ Bc.T
     d2 = np.maximum(np.diag(gc)[:, None] + np.diag(gc)[None, :] - 2 * gc, 0.0)
     got = np.diag(G)[:, None] + np.diag(G)[None, :] - 2 * G
-    np.testing.assert_allclose(got, d2, rtol=2e-5, atol=1e-9 * d2.max())
+    # the means' spread is a third of the rows' while the Byzantine offset is
+    # not, so the nearest pairs cancel more of G_ii + G_jj - 2 G_ij: the score
+    # tolerance (SCORE_RTOL), not the raw-row Gram test's 2e-5
+    np.testing.assert_allclose(got, d2, rtol=SCORE_RTOL, atol=1e-9 * d2.max())
     order, _ = engine.krum_from_gram(torch.from_numpy(G).cuda(), f, 1, scores=False)
     want = int(np.argmin(orc.krum_(list(B.astype(np.float32)), f)))
     assert int(order.cpu()[0]) == want
