@@ -526,7 +526,12 @@ def main():
 
     bound, peak, unit, alg = roofline_model(a.agg, n, d)
     solver_note = None
-    if a.agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
+    n_filter = engine.mom_bucket_count(n, FILTER_ARGS["eps"], MOM_DELTA)[0] if a.agg.startswith("mom_") else n
+    if a.agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret") and n_filter > 128:
+        # the debug records (sra_filter_debug_f32) exist for the register solver
+        # only (N <= 128): above it the flops are the chunk Grams alone
+        solver_note = "chunk Grams n(n+1)d only (N > 128: no per-step records for the solver)"
+    elif a.agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
         sflops, iters = solver_flops(a.agg, X)
         alg = alg + int(sflops)
         solver_note = "chunk Grams n(n+1)d + solver %.3g flop (chunk 0: %d iterations, its Lanczos steps)%s" % (
