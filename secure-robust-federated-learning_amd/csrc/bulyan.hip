@@ -329,8 +329,9 @@ __global__ void __launch_bounds__(256) select_rows_lds_kernel(const float* __res
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int64_t j0 = static_cast<int64_t>(blockIdx.x) * tile;
   const int tid = threadIdx.x;
+  const int lt = __builtin_ctz(static_cast<unsigned>(tile));
   for (int e = tid; e < pn * tile; e += blockDim.x) {
-    const int r = e / tile, c = e - r * tile;
+    const int r = e >> lt, c = e & (tile - 1);   // tile: a power of two
     const int64_t j = j0 + c;
     float x = qnan();
     if (r < n && j < d) {
@@ -343,9 +344,9 @@ __global__ void __launch_bounds__(256) select_rows_lds_kernel(const float* __res
   for (int k = 2; k <= pn; k <<= 1) {
     for (int s = k >> 1; s > 0; s >>= 1) {
       for (int q = tid; q < pairs; q += blockDim.x) {
-        const int c = q % tile;
-        const int h = q / tile;
-        const int i = ((h / s) * (2 * s)) + (h % s);
+        const int c = q & (tile - 1);
+        const int h = q >> lt;
+        const int i = h + (h & ~(s - 1));   // (h / s) * 2s + h % s, s a power of two
         const int l = i + s;
         float a = lds[i * tile + c], b = lds[l * tile + c];
         if ((i & k) == 0) ce(a, b); else ce(b, a);
@@ -938,7 +939,7 @@ __global__ void __launch_bounds__(256) bulyan_final_lds_kernel(const float* __re
       for (int q = tid; q < pairs; q += blockDim.x) {
         const int c = q & (TW - 1);
         const int h = q >> LG;
-        const int i = ((h / s) * (2 * s)) + (h % s);
+        const int i = h + (h & ~(s - 1));   // (h / s) * 2s + h % s, s a power of two
         const int l = i + s;
         float a = colt[i * TW + c], b = colt[l * TW + c];
         if ((i & k) == 0) ce(a, b); else ce(b, a);

@@ -500,9 +500,10 @@ __global__ void __launch_bounds__(256) select_lds_kernel(const float* __restrict
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int64_t j0 = static_cast<int64_t>(blockIdx.x) * tile;
   const int tid = threadIdx.x;
+  const int lt = __builtin_ctz(static_cast<unsigned>(tile));   // tile: a power of two
   // load: row-major sweep, consecutive lanes -> consecutive coordinates
   for (int e = tid; e < pn * tile; e += blockDim.x) {
-    const int r = e / tile, c = e - r * tile;
+    const int r = e >> lt, c = e & (tile - 1);
     const int64_t j = j0 + c;
     float x = qnan();
     if (r < n && j < d) x = X[(int64_t)r * ldx + j];
@@ -513,9 +514,9 @@ __global__ void __launch_bounds__(256) select_lds_kernel(const float* __restrict
   for (int k = 2; k <= pn; k <<= 1) {
     for (int s = k >> 1; s > 0; s >>= 1) {
       for (int q = tid; q < pairs; q += blockDim.x) {
-        const int c = q % tile;
-        const int h = q / tile;                            // pair index within the column
-        const int i = ((h / s) * (2 * s)) + (h % s);       // lower element of the pair
+        const int c = q & (tile - 1);
+        const int h = q >> lt;                             // pair index within the column
+        const int i = h + (h & ~(s - 1));   // lower element of the pair: (h / s) * 2s + h % s
         const int l = i + s;
         float a = lds[i * tile + c], b = lds[l * tile + c];
         if ((i & k) == 0) ce(a, b); else ce(b, a);
@@ -687,8 +688,9 @@ __global__ void __launch_bounds__(256) order_stat_lds_kernel(const float* __rest
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [pn][tile]
   const int64_t j0 = static_cast<int64_t>(blockIdx.x) * tile;
   const int tid = threadIdx.x;
+  const int lt = __builtin_ctz(static_cast<unsigned>(tile));   // tile: a power of two
   for (int e = tid; e < pn * tile; e += blockDim.x) {
-    const int r = e / tile, c = e - r * tile;
+    const int r = e >> lt, c = e & (tile - 1);
     const int64_t j = j0 + c;
     lds[e] = (r < n && j < d) ? X[static_cast<int64_t>(r) * ldx + j] : qnan();
   }
@@ -697,9 +699,9 @@ __global__ void __launch_bounds__(256) order_stat_lds_kernel(const float* __rest
   for (int kk = 2; kk <= pn; kk <<= 1) {
     for (int st = kk >> 1; st > 0; st >>= 1) {
       for (int q = tid; q < pairs; q += blockDim.x) {
-        const int c = q % tile;
-        const int h = q / tile;
-        const int i = ((h / st) * (2 * st)) + (h % st);
+        const int c = q & (tile - 1);
+        const int h = q >> lt;
+        const int i = h + (h & ~(st - 1));   // (h / st) * 2st + h % st, st a power of two
         const int l = i + st;
         float a = lds[i * tile + c], b = lds[l * tile + c];
         if ((i & kk) == 0) ce(a, b); else ce(b, a);
