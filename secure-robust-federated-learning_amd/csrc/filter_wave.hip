@@ -1,0 +1,741 @@
+// k6, round 5 — the spectral filters' one-wave solver (filterL2 and its MoM
+// form; replaces the four-wave lanczos_solve_kernel).
+//
+// Reference: src/robust_estimator.py:144-175 (filterL2_: 2*int(eps*n)
+// iterations of: weighted mean and covariance, top eigenpair by eigh, early
+// exit if lambda^2 <= expansion * sigma^2, tau = ((x - mu).v)^2, c *= 1 -
+// tau / tau_max, drop the argmax, c /= |c|_1) and :177-208 (the itv chunks).
+//
+// Client space as before: with w = c / sum(c), the weighted
+// covariance's nonzero spectrum is that of M = W^1/2 C W^1/2, C the Gram of
+// the rows centred at the weighted mean, and tau_i = (C W^1/2 u)_i^2 / lambda
+// for M's top eigenpair (lambda, u).  What is new:
+//
+//  * ONE wave per chunk, four per CU (one per SIMD).  C is held in the
+//    circulant-half form of wave_sym.hpp (lane l: rows 2l and 2l + 1, the 65
+//    diagonals k = 0 .. 64; WKV of them in VGPRs, the rest in LDS), so a
+//    matvec is 130 + 126 fp64 fmas and 126 DPP moves per lane, and every
+//    reduction of the Lanczos step, the checks and the filter decision is a
+//    DPP / readlane wave reduction: no workgroup barrier anywhere (the
+//    four-wave solver paid two block reductions per Lanczos step, two
+//    workgroups per CU).
+//  * C is recentred in place every iteration instead of being rebuilt from
+//    the chunk Gram G: with g = C w and s = w'g, C <- C - g 1' - 1 g' + s 1 1'
+//    is (I - 1 w')C(I - w 1'), the Gram centred at the new weighted mean,
+//    because (I - 1 w')(I - 1 w_old') = I - 1 w' when w'1 = 1.  G is read
+//    once per chunk (the four-wave solver re-read its 128 KiB every
+//    iteration: 78.6 GB per C4 call), and the entries stay centred at the
+//    current weights, so forming them never cancels the offset of the
+//    unweighted mean.  M is applied as W^1/2 C W^1/2 x (two scalings per
+//    lane around the matvec).
+//  * Lanczos basis vectors go to a per-wave global scratch (1 KiB per step,
+//    off the step's critical path; read back once per iteration for the
+//    Ritz vector).
+//
+// The Lanczos schedule is the four-wave solver's (plain three-term Lanczos,
+// checks at residual-decay-extrapolated steps, acceptance at 2.5e-16 lambda,
+// a ghost retries once with dense checks, then a re-orthogonalising attempt
+// in the same kernel; a chunk that still fails is listed for
+// filter_solve_kernel).  The check (top eigenpair of T_m) is fast_check's
+// algorithm in one wave: Laguerre from the Gershgorin bound, multisection
+// over 64 Sturm points per round, the two eigenvector recurrences of
+// (T - theta) f = 0 interleaved in one instruction stream, the twist.
+#include "filter_common.hpp"
+#include "sra_common.hpp"
+#include "wave_sym.hpp"
+
+namespace sra {
+
+constexpr int WKV = 40;                       // C's diagonals in VGPRs (tools/ubench/wave_step.hip: 32 / 40 / 48)
+constexpr int WKL = wsym::NK - WKV;           // ... in LDS
+constexpr int kExStride = 72;                 // check: exponents per block of 4 chain steps, per chain
+constexpr int kWScr = 4 * MMAX + 2 * kExStride;   // operand (256) + group shifts (384) | check scratch
+static_assert(kWScr >= wsym::kZd + wsym::kTb, "the check scratch overlays the matvec scratch");
+constexpr int kWTrw = 2 * MMAX + 32;          // T record: (alpha_q, beta^2_{q-1}) pairs + prefetch padding
+constexpr size_t kWaveLds = sizeof(double) * (static_cast<size_t>(WKL) * FNP + kWScr + kWTrw + 2 * MMAX);
+static_assert(4 * kWaveLds <= 163840, "four one-wave solvers must fit one CU's LDS");
+constexpr int kWaveGrid = 1024;               // 4 waves per CU x 256 CUs; each owns a basis slot
+
+// ---- the check: top Ritz pair of T_m in one wave ---------------------------
+// T: LDS record, T[2q] = alpha_q, T[2q+1] = beta^2 of (q-1, q) (T[1] = 0).
+// Returns theta (2-ulp bracket midpoint), the last component of the
+// normalised eigenvector (the residual is beta_m |z_{m-1}|), and writes z[0, m).
+__device__ __forceinline__ void wave_check(const double* T, int m, double theta_lb, double hint, double glo,
+                                           double ghi, double* z, double* scr, double* theta_out,
+                                           double* zlast_out, int* rounds_out) {
+  m = __builtin_amdgcn_readfirstlane(m);
+  const int lane = threadIdx.x & 63;
+  double* gq = scr;                  // [MMAX] g | [MMAX] Q  (forward chain)
+  double* hr = scr + 2 * MMAX;       // [MMAX] h | [MMAX] R  (backward chain)
+  double* ex = scr + 4 * MMAX;       // [kExStride] forward exponents | [kExStride] backward
+  const double a0 = T[0];
+  double lo = fmax(glo, fmax(theta_lb, a0));
+  double hi = ghi;
+  if (!(lo < hi)) lo = glo;
+  const bool hinted = hint >= 0.0 && theta_lb > -1e299;
+  const double hg = lo + 4.0 * hint + 4e-16 * fabs(lo);
+  const double2* T2 = reinterpret_cast<const double2*>(T);
+  // Sturm count at x: the number of eigenvalues below x (>= m: x is above all)
+  auto count = [&](double x) -> int {
+    double p2 = 1.0, p1 = a0 - x;
+    unsigned cnt = static_cast<unsigned>(__builtin_bit_cast(unsigned long long, p1) >> 63);
+    auto step = [&](double2 t) __attribute__((always_inline)) {
+      const double pk = fma(t.x - x, p1, -(t.y * p2));
+      cnt += static_cast<unsigned>((__builtin_bit_cast(unsigned long long, pk) ^
+                                    __builtin_bit_cast(unsigned long long, p1)) >> 63);
+      p2 = p1;
+      p1 = pk;
+    };
+    double2 c0 = T2[1], c1 = T2[2];
+    int q = 1;
+    for (; q + 4 <= m; q += 4) {
+      const double2 c2 = T2[q + 2], c3 = T2[q + 3];
+      step(c0);
+      step(c1);
+      c0 = T2[q + 4];
+      c1 = T2[q + 5];
+      step(c2);
+      step(c3);
+      const int e = __builtin_amdgcn_frexp_exp(p1);
+      p1 = __builtin_amdgcn_ldexp(p1, -e);
+      p2 = __builtin_amdgcn_ldexp(p2, -e);
+    }
+    if (q < m) step(c0);
+    if (q + 1 < m) step(c1);
+    if (q + 2 < m) step(T2[q + 2]);
+    return static_cast<int>(cnt);
+  };
+  // cold start: Laguerre from the Gershgorin upper bound (fast_check)
+  bool laguerre = false;
+  const double lo0 = lo, hi0 = hi;
+  if (!hinted && m > 2) {
+    double x = hi;
+    for (int itl = 0; itl < 16; ++itl) {
+      double p0 = 1.0, p1 = x - a0, d0 = 0.0, d1 = 1.0, e0 = 0.0, e1 = 0.0;
+      auto lstep = [&](double2 t) __attribute__((always_inline)) {
+        const double c = x - t.x;
+        const double pn = fma(c, p1, -(t.y * p0));
+        const double dn = fma(c, d1, p1 - t.y * d0);
+        const double en = fma(c, e1, 2.0 * d1 - t.y * e0);
+        p0 = p1; p1 = pn;
+        d0 = d1; d1 = dn;
+        e0 = e1; e1 = en;
+      };
+      double2 c0 = T2[1], c1 = T2[2];
+      int q = 1;
+      for (; q + 4 <= m; q += 4) {
+        const double2 c2 = T2[q + 2], c3 = T2[q + 3];
+        lstep(c0);
+        lstep(c1);
+        c0 = T2[q + 4];
+        c1 = T2[q + 5];
+        lstep(c2);
+        lstep(c3);
+        const int e = __builtin_amdgcn_frexp_exp(fmax(fabs(p1), fabs(d1)));
+        p0 = __builtin_amdgcn_ldexp(p0, -e); p1 = __builtin_amdgcn_ldexp(p1, -e);
+        d0 = __builtin_amdgcn_ldexp(d0, -e); d1 = __builtin_amdgcn_ldexp(d1, -e);
+        e0 = __builtin_amdgcn_ldexp(e0, -e); e1 = __builtin_amdgcn_ldexp(e1, -e);
+      }
+      if (q < m) lstep(c0);
+      if (q + 1 < m) lstep(c1);
+      if (q + 2 < m) lstep(T2[q + 2]);
+      if (!(p1 != 0.0)) break;
+      const double G = d1 / p1, H = G * G - e1 / p1;
+      const double nn = static_cast<double>(m);
+      const double den = G + sqrt(fmax((nn - 1.0) * (nn * H - G * G), 0.0));
+      const double xn = x - nn / den;
+      if (!(xn < x) || !(xn >= lo0)) break;
+      const bool fin = x - xn <= 4e-16 * fabs(x);
+      x = xn;
+      if (fin) break;
+    }
+    const double u = 64.0 * 2.2204460492503131e-16 * fabs(x);
+    if (x - u > lo0 && x + u < hi0) {
+      lo = x - u;
+      hi = x + u;
+      laguerre = true;
+    }
+  }
+  // multisection: 64 Sturm points per round, one per lane
+  int round = 0;
+  for (; round < 48; ++round) {
+    const int kind = round == 0 ? (laguerre ? 3 : (hinted && hg < hi ? 1 : 2)) : 0;
+    const double rlo = lo, rhi = hi;
+    auto point = [&](int p) -> double {
+      if (kind == 1) return p < 63 ? rlo + (hg - rlo) * ((p + 1) * (1.0 / 63.0)) : rhi;
+      if (kind == 2) return rlo + (rhi - rlo) * __builtin_amdgcn_ldexp(1.0, p - 63);
+      if (kind == 3) return rlo + (rhi - rlo) * (p * (1.0 / 63.0));
+      return rlo + (rhi - rlo) * ((p + 1) * (1.0 / 65.0));
+    };
+    const unsigned long long ok = __builtin_amdgcn_ballot_w64(count(point(lane)) >= m);
+    const int first = ok ? __builtin_ctzll(ok) : 64;
+    if (kind == 3 && (first == 0 || first == 64)) {
+      lo = lo0;
+      hi = hi0;
+      laguerre = false;
+      continue;
+    }
+    const double xf = first < 64 ? point(first) : rhi;
+    const double xb = first > 0 ? point(first - 1) : rlo;
+    const bool stalled = xb == lo && xf == hi;
+    lo = xb;
+    hi = xf;
+    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
+  }
+  const double lm = 0.5 * (lo + hi);
+  // ---- the two eigenvector recurrences of (T - lm) f = 0 in the division-
+  // free minor form (fast_check), forward from the top and backward from the
+  // bottom, interleaved; rescaled by powers of two every four steps
+  {
+    double* exf = ex;
+    double* exb = ex + kExStride;
+    double fg1 = 1.0, fg0 = 0.0, fq = 1.0, bg1 = 1.0, bg0 = 0.0, bq = 1.0, bbw = 0.0;
+    int feg = 0, feq = 0, beg = 0, beq = 0;
+    double fgv[2] = {0.0, 0.0}, fqv[2] = {0.0, 0.0}, bgv[2] = {0.0, 0.0}, bqv[2] = {0.0, 0.0};
+    if (lane == 0) {
+      fgv[0] = 1.0;
+      fqv[0] = 1.0;
+      exf[0] = exf[1] = exb[0] = exb[1] = 0.0;
+    }
+    if (((m - 1) & 63) == lane) {
+      if (m - 1 < 64) {
+        bgv[0] = 1.0;
+        bqv[0] = 1.0;
+      } else {
+        bgv[1] = 1.0;
+        bqv[1] = 1.0;
+      }
+    }
+    auto put = [&](double (&gv)[2], double (&qv)[2], int idx, double g, double q) __attribute__((always_inline)) {
+      const bool me = (idx & 63) == lane;
+      if (idx < 64) {
+        gv[0] = me ? g : gv[0];
+        qv[0] = me ? q : qv[0];
+      } else {
+        gv[1] = me ? g : gv[1];
+        qv[1] = me ? q : qv[1];
+      }
+    };
+    // fwd row i = k: (alpha_k, behind beta^2_{k-1}), ahead beta^2_k; index k + 1
+    // bwd row i = m-1-k: alpha_i, ahead beta^2_{i-1} = T2[i].y, behind the
+    // previous pair's .y; index m - 2 - k
+    auto step = [&](int k) __attribute__((always_inline)) {
+      const double2 fc = T2[k], fn = T2[k + 1], bc = T2[m - 1 - k];
+      const double fgn = fma(lm - fc.x, fg1, -(fc.y * fg0));
+      fq *= fn.y;
+      fg0 = fg1;
+      fg1 = fgn;
+      const double bgn = fma(lm - bc.x, bg1, -(bbw * bg0));
+      bq *= bc.y;
+      bbw = bc.y;
+      bg0 = bg1;
+      bg1 = bgn;
+    };
+    auto rescale = [&](int k) __attribute__((always_inline)) {
+      int e = __builtin_amdgcn_frexp_exp(fg1);
+      fg1 = __builtin_amdgcn_ldexp(fg1, -e);
+      fg0 = __builtin_amdgcn_ldexp(fg0, -e);
+      feg += e;
+      e = __builtin_amdgcn_frexp_exp(fq);
+      fq = __builtin_amdgcn_ldexp(fq, -e);
+      feq += e;
+      e = __builtin_amdgcn_frexp_exp(bg1);
+      bg1 = __builtin_amdgcn_ldexp(bg1, -e);
+      bg0 = __builtin_amdgcn_ldexp(bg0, -e);
+      beg += e;
+      e = __builtin_amdgcn_frexp_exp(bq);
+      bq = __builtin_amdgcn_ldexp(bq, -e);
+      beq += e;
+      if (lane == 0) {
+        const int b = 2 * ((k + 1) >> 2);
+        exf[b] = static_cast<double>(feg);
+        exf[b + 1] = static_cast<double>(feq);
+        exb[b] = static_cast<double>(beg);
+        exb[b + 1] = static_cast<double>(beq);
+      }
+    };
+    const int steps = m - 1;
+    int k = 0;
+    for (; k + 4 <= steps; k += 4) {
+      step(k);
+      put(fgv, fqv, k + 1, fg1, fq);
+      put(bgv, bqv, m - 2 - k, bg1, bq);
+      step(k + 1);
+      put(fgv, fqv, k + 2, fg1, fq);
+      put(bgv, bqv, m - 3 - k, bg1, bq);
+      step(k + 2);
+      put(fgv, fqv, k + 3, fg1, fq);
+      put(bgv, bqv, m - 4 - k, bg1, bq);
+      step(k + 3);
+      rescale(k + 3);
+      put(fgv, fqv, k + 4, fg1, fq);
+      put(bgv, bqv, m - 5 - k, bg1, bq);
+    }
+    for (; k < steps; ++k) {
+      step(k);
+      put(fgv, fqv, k + 1, fg1, fq);
+      put(bgv, bqv, m - 2 - k, bg1, bq);
+    }
+    gq[lane] = fgv[0];
+    gq[64 + lane] = fgv[1];
+    gq[MMAX + lane] = fqv[0];
+    gq[MMAX + 64 + lane] = fqv[1];
+    hr[lane] = bgv[0];
+    hr[64 + lane] = bgv[1];
+    hr[MMAX + lane] = bqv[0];
+    hr[MMAX + 64 + lane] = bqv[1];
+  }
+  wsym::lds_order();   // every lane reads its neighbours' chain values
+  auto pexp = [&](const double* exb, int p, int which) -> int { return static_cast<int>(exb[2 * (p >> 2) + which]); };
+  const double* exf = ex;
+  const double* exb = ex + kExStride;
+  // ---- gamma, twist (first index of the smallest |gamma|), z
+  double zv[2], gam = 1e308;
+  int tw = 0;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int k = lane + 64 * s2;
+    zv[s2] = 0.0;
+    if (k < m) {
+      double g = T[2 * k] - lm;
+      if (k > 0)
+        g += T[2 * k + 1] * __builtin_amdgcn_ldexp(gq[k - 1] * rcp_nr(gq[k]), pexp(exf, k - 1, 0) - pexp(exf, k, 0));
+      if (k + 1 < m)
+        g += T[2 * k + 3] *
+             __builtin_amdgcn_ldexp(hr[k + 1] * rcp_nr(hr[k]), pexp(exb, m - 2 - k, 0) - pexp(exb, m - 1 - k, 0));
+      const double ga = fabs(g);
+      if (ga < gam) {
+        gam = ga;
+        tw = k;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double og = __shfl_xor(gam, off);
+    const int ot = __shfl_xor(tw, off);
+    if (og < gam || (og == gam && ot < tw)) {
+      gam = og;
+      tw = ot;
+    }
+  }
+  tw = __builtin_amdgcn_readfirstlane(tw);
+  const double igr = rcp_nr(gq[tw]), ihr = rcp_nr(hr[tw]);
+  const double qr = gq[MMAX + tw], rr = hr[MMAX + tw];
+  const int egr = pexp(exf, tw, 0), eqr = pexp(exf, tw, 1);
+  const int ehr = pexp(exb, m - 1 - tw, 0), err = pexp(exb, m - 1 - tw, 1);
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int k = lane + 64 * s2;
+    if (k < m) {
+      if (k <= tw) {   // (g_k / g_r) sqrt(Q_r / Q_k)
+        int e2 = eqr - pexp(exf, k, 1);
+        double qratio = qr * rcp_nr(gq[MMAX + k]);
+        if (e2 & 1) { qratio *= 2.0; e2 -= 1; }
+        zv[s2] = __builtin_amdgcn_ldexp(gq[k] * igr * sqrt(qratio), pexp(exf, k, 0) - egr + e2 / 2);
+      } else {         // (h_k / h_r) sqrt(R_r / R_k)
+        int e2 = err - pexp(exb, m - 1 - k, 1);
+        double rratio = rr * rcp_nr(hr[MMAX + k]);
+        if (e2 & 1) { rratio *= 2.0; e2 -= 1; }
+        zv[s2] = __builtin_amdgcn_ldexp(hr[k] * ihr * sqrt(rratio), pexp(exb, m - 1 - k, 0) - ehr + e2 / 2);
+      }
+    }
+  }
+  const double inv = 1.0 / sqrt(wave_sum(zv[0] * zv[0] + zv[1] * zv[1]));
+  if (lane < m) z[lane] = zv[0] * inv;
+  if (lane + 64 < m) z[lane + 64] = zv[1] * inv;
+  wsym::lds_order();
+  *zlast_out = rl_any(zv, m - 1) * inv;
+  *theta_out = lm;
+  *rounds_out = round + 1;
+}
+
+// ---- C <- C - g 1' - 1 g' + s 1 1' on the packed form ----------------------
+// zd holds g doubled; ri_s = s - g_row.  Entry (m, m + k): (C + ri) - g_{m+k}
+template <int KV>
+__device__ __forceinline__ void recentre(wsym::Packed<KV>& P, double* cl, const double* zd, double ri0, double ri1) {
+  const int lane = threadIdx.x & 63;
+  const double2* xp = reinterpret_cast<const double2*>(zd) + lane;
+  wsym::sfor<wsym::NK>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    constexpr int j = k / 2;
+    double gj0, gj1;
+    if constexpr ((k & 1) == 0) {
+      const double2 X = xp[j];
+      gj0 = X.x;
+      gj1 = X.y;
+    } else {
+      gj0 = xp[j].y;
+      gj1 = xp[j + 1].x;
+    }
+    if constexpr (k < KV) {
+      P.cv[k][0] = (P.cv[k][0] + ri0) - gj0;
+      P.cv[k][1] = (P.cv[k][1] + ri1) - gj1;
+    } else {
+      double2* c = reinterpret_cast<double2*>(cl + (k - KV) * FNP) + lane;
+      const double2 v = *c;
+      *c = double2{(v.x + ri0) - gj0, (v.y + ri1) - gj1};
+    }
+  });
+}
+
+// first index of the largest value over the wave (value, index) pairs
+__device__ __forceinline__ int wave_argmax_first(double v, int i, double* vbest) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const int oi = __shfl_xor(i, off);
+    if (ov > v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  *vbest = readlane_f64(v, 0);
+  return __builtin_amdgcn_readfirstlane(i);
+}
+
+template <int MODE, bool DBG>
+__global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
+  static_assert(MODE == 0, "ex_noregret stays on filter_solve_kernel");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* cl = reinterpret_cast<double*>(smem);   // [WKL][FNP] C's LDS diagonals
+  double* scr = cl + WKL * FNP;                   // [kWScr] operand + group shifts | check scratch
+  double* zd = scr;
+  double* tb = scr + wsym::kZd;
+  double* trw = scr + kWScr;                      // [kWTrw] tridiagonal record
+  double* zbuf = trw + kWTrw;                     // [2][MMAX] eigenvectors of T (current / best check)
+  const int lane = threadIdx.x;
+  const int r0 = 2 * lane, r1 = r0 + 1;
+  const int n = A.n;
+  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * MMAX * FNP;
+  if (lane < 32) trw[2 * MMAX + lane] = 0.0;   // prefetch padding of the T record
+  if (lane == 0) trw[1] = 0.0;                   // beta^2_{-1}: multiplies a zero in the check's forward chain
+
+  for (;;) {
+    int ch = lane == 0 ? atomicAdd(A.fb_count + 4, 1) : 0;
+    ch = __builtin_amdgcn_readfirstlane(ch);
+    if (ch >= A.nb) break;
+    const bool dbg = DBG && ch == 0;
+    // ---- C = G (the chunk Gram, centred at the unweighted mean) into the packed form
+    wsym::Packed<WKV> P;
+    {
+      const double* Gc = A.G + static_cast<size_t>(ch) * FNP * FNP;
+      wsym::sfor<wsym::NK>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        const double v0 = Gc[r0 * FNP + ((r0 + k) & (FNP - 1))];
+        const double v1 = Gc[r1 * FNP + ((r1 + k) & (FNP - 1))];
+        if constexpr (k < WKV) {
+          P.cv[k][0] = v0;
+          P.cv[k][1] = v1;
+        } else {
+          reinterpret_cast<double2*>(cl + (k - WKV) * FNP)[lane] = double2{v0, v1};
+        }
+      });
+    }
+    bool ai0 = r0 < n, ai1 = r1 < n;
+    double ci0 = ai0 ? 1.0 : 0.0, ci1 = ai1 ? 1.0 : 0.0;
+    const int iters = 2 * static_cast<int>(A.eps * n);
+    int m_hint = 24;
+    double rate_hint = 0.0;
+    bool fallback = false;
+    int done = 0;
+    int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
+    const double hh0 = 0.5 + (r0 * 0.6180339887498949 - floor(r0 * 0.6180339887498949));
+    const double hh1 = 0.5 + (r1 * 0.6180339887498949 - floor(r1 * 0.6180339887498949));
+
+    for (int it = 0; it < iters; ++it) {
+      const long long t_it = dbg ? clock64() : 0;
+      // ---- weights, and C recentred at the weighted mean
+      const double csum = wave_sum((ai0 ? ci0 : 0.0) + (ai1 ? ci1 : 0.0));
+      const int nact = static_cast<int>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(ai0)) +
+                                        __builtin_popcountll(__builtin_amdgcn_ballot_w64(ai1)));
+      const double w0 = ai0 ? ci0 / csum : 0.0, w1 = ai1 ? ci1 / csum : 0.0;
+      const double sw0 = sqrt(w0 > 0.0 ? w0 : 0.0), sw1 = sqrt(w1 > 0.0 ? w1 : 0.0);
+      double sgw;
+      {
+        double g0, g1;
+        wsym::put_operand(zd, w0, w1);
+        wsym::matvec<WKV>(P, cl, zd, tb, w0, w1, g0, g1);
+        sgw = wave_sum(w0 * g0 + w1 * g1);
+        wsym::put_operand(zd, g0, g1);
+        recentre<WKV>(P, cl, zd, sgw - g0, sgw - g1);
+      }
+
+      // ---- top eigenpair of M = W^1/2 C W^1/2 by plain Lanczos
+      double lam = 0.0, resid = 0.0, u0 = 0.0, u1 = 0.0;
+      int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
+      bool converged = false;
+      double tscale = 0.0;
+      long long tcheck = 0, tmv = 0, tstep = 0;
+      int trounds = 0;
+      // attempt 0: plain Lanczos; 1: after a ghost, again with dense checks;
+      // 2: with full re-orthogonalisation against the stored basis
+      for (int attempt = 0; attempt < 3 && !converged; ++attempt) {
+        const bool reorth = attempt == 2;
+        double rt0 = sw0 > 0.0 ? sw0 * hh0 : 0.0, rt1 = sw1 > 0.0 ? sw1 * hh1 : 0.0;
+        double nrm2 = wave_sum(rt0 * rt0 + rt1 * rt1);
+        double qp0 = 0.0, qp1 = 0.0, theta_lb = -1e300, hint = -1.0;
+        double res_best = 1e300, lam_best = 0.0;
+        tscale = 0.0;
+        double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
+        const int adv_max = attempt == 1 ? 1 : A.max_adv;
+        const int first = m_hint + A.first_off > 4 ? m_hint + A.first_off : 4;
+        int next_check = attempt == 1 ? (m_retry > 4 ? m_retry : 4) : first;
+        int m_a = -1, m_last = 4, m_pre = 4;
+        double res_a = 0.0;
+        bool ghost = false;
+        for (int j = 0;; ++j) {
+          const double bet = sqrt(nrm2);
+          if (j > 0) {
+            trw[2 * j + 1] = nrm2;   // every lane stores the same value: no exec-mask branch
+            tscale = fmax(tscale, bet);
+            const bool breakdown = !(bet > 1e-14 * tscale);
+            if (breakdown || j == MMAX || j >= next_check) {
+              const int m = j;
+              wsym::lds_order();   // lane 0's T record entries
+              ++nchecks;
+              const long long tc0 = dbg ? clock64() : 0;
+              double lm, zl;
+              int rounds = 0;
+              const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
+              wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, scr, &lm, &zl, &rounds);
+              if (dbg) {
+                tcheck += clock64() - tc0;
+                trounds += rounds;
+              }
+              const double res = fabs(bet * zl);
+              hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
+              theta_lb = lm;
+              if (res <= kAccept * fabs(lm) || breakdown) {
+                converged = true;
+                m_conv = m;
+                lam = lm;
+                resid = res;
+                zbest = zcur;
+                break;
+              }
+              if (res < res_best) {
+                m_pre = m_last;
+                res_best = res;
+                lam_best = lm;
+                zbest = zcur;
+                zcur ^= 1;
+              }
+              ghost = !reorth && res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
+              const bool out_of_steps = j == MMAX;
+              if (ghost || out_of_steps) {
+                if (lane == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
+                if (!ghost && attempt < 2) {   // out of steps: straight on to the re-orthogonalising attempt
+                  ghost = true;
+                  attempt = 1;
+                }
+                m_retry = m_pre;
+                break;
+              }
+              int adv = 4;
+              double rate = rate_hint;
+              if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
+              if (rate < 0.0 && res > 0.0) {
+                const double need = log(kAccept * fabs(lm) / res) / rate;
+                adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
+              }
+              m_a = m;
+              res_a = res;
+              m_last = m;
+              next_check = m + adv;
+            }
+            gfin_hi = fmax(gfin_hi, a_last + b_prev + bet);
+            gfin_lo = fmin(gfin_lo, a_last - b_prev - bet);
+            b_prev = bet;
+          }
+          // y = M r~ (r~ = beta q_j), alpha_j = q_j . M q_j
+          const long long ts0 = dbg ? clock64() : 0;
+          double y0, y1;
+          {
+            const double z0 = sw0 * rt0, z1 = sw1 * rt1;
+            wsym::put_operand(zd, z0, z1);
+            wsym::matvec<WKV>(P, cl, zd, tb, z0, z1, y0, y1);
+          }
+          const long long ts1 = dbg ? clock64() : 0;
+          if (dbg) tmv += ts1 - ts0;
+          const double ib = 1.0 / bet;
+          const double q0 = rt0 * ib, q1 = rt1 * ib;
+          reinterpret_cast<double2*>(Vb + j * FNP)[lane] = double2{q0, q1};
+          const double mq0 = sw0 * y0 * ib, mq1 = sw1 * y1 * ib;
+          double aj = wave_sum(q0 * mq0 + q1 * mq1);
+          double n0 = mq0 - aj * q0 - (j > 0 ? bet * qp0 : 0.0);
+          double n1 = mq1 - aj * q1 - (j > 0 ? bet * qp1 : 0.0);
+          if (reorth) {
+            // classical Gram-Schmidt against q_0 .. q_j (read back from the
+            // scratch after the stores landed), a second pass when |r|^2
+            // drops below half (DGKS); alpha takes the q_j coefficients
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const double2* V2 = reinterpret_cast<const double2*>(Vb);
+            double* hb = tb;   // [MMAX + 2] coefficients (the matvec scratch is free until the next step)
+            for (int pass = 0; pass < 2; ++pass) {
+              const int nh = pass == 0 ? j + 2 : j + 1;
+              for (int qq = 0; qq < nh; ++qq) {
+                double v;
+                if (qq <= j) {
+                  const double2 b = V2[qq * 64 + lane];
+                  v = b.x * n0 + b.y * n1;
+                } else {
+                  v = n0 * n0 + n1 * n1;
+                }
+                v = wave_sum(v);
+                if (lane == 0) hb[qq] = v;
+              }
+              wsym::lds_order();
+              double up0 = 0.0, up1 = 0.0, hn2 = 0.0;
+              for (int qq = 0; qq <= j; ++qq) {
+                const double hv = hb[qq];
+                const double2 b = V2[qq * 64 + lane];
+                up0 = fma(hv, b.x, up0);
+                up1 = fma(hv, b.y, up1);
+                hn2 = fma(hv, hv, hn2);
+              }
+              n0 -= up0;
+              n1 -= up1;
+              aj += hb[j];
+              const bool again = pass == 0 && hb[j + 1] - hn2 < kDgks * hb[j + 1];
+              wsym::lds_order();
+              if (!again) break;
+            }
+          }
+          trw[2 * j] = aj;   // every lane: no exec-mask branch
+          a_last = aj;
+          tscale = fmax(tscale, fabs(aj));
+          qp0 = q0;
+          qp1 = q1;
+          rt0 = n0;
+          rt1 = n1;
+          nrm2 = wave_sum(n0 * n0 + n1 * n1);
+          if (dbg) tstep += clock64() - ts1;
+        }
+        if (!ghost) break;
+      }
+      if (!converged) {
+        fallback = true;
+        break;
+      }
+      // ---- Ritz vector u = V z of the accepted check
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // also orders the check's z writes before the reads
+      {
+        const double* zb = zbuf + zbest * MMAX;
+        const double2* V2 = reinterpret_cast<const double2*>(Vb);
+        double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+        int qq = 0;
+        for (; qq + 1 < m_conv; qq += 2) {
+          const double za = zb[qq], zb1 = zb[qq + 1];
+          const double2 va = V2[qq * 64 + lane], vb = V2[(qq + 1) * 64 + lane];
+          a0 = fma(za, va.x, a0);
+          a1 = fma(za, va.y, a1);
+          b0 = fma(zb1, vb.x, b0);
+          b1 = fma(zb1, vb.y, b1);
+        }
+        if (qq < m_conv) {
+          const double za = zb[qq];
+          const double2 va = V2[qq * 64 + lane];
+          a0 = fma(za, va.x, a0);
+          a1 = fma(za, va.y, a1);
+        }
+        u0 = sw0 > 0.0 ? a0 + b0 : 0.0;
+        u1 = sw1 > 0.0 ? a1 + b1 : 0.0;
+      }
+      m_hint = m_conv > 8 ? m_conv : 8;
+      if (dbg && it < 256) {
+        double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
+        reinterpret_cast<double2*>(rec)[lane] = double2{ci0, ci1};
+        if (lane == 0) {
+          rec[FNP] = lam;
+          rec[FNP + 1] = m_conv;
+          rec[FNP + 2] = resid;
+          rec[FNP + 3] = nchecks;
+          rec[FNP + 4] = nact;
+          rec[FNP + 5] = sgw;
+          rec[FNP + 6] = 0;
+          rec[FNP + 7] = 0;
+          rec[FNP + 8] = static_cast<double>(clock64() - t_it);
+          rec[FNP + 9] = static_cast<double>(tcheck);
+          rec[FNP + 10] = static_cast<double>(tmv);
+          rec[FNP + 11] = static_cast<double>(tstep);
+          rec[FNP + 12] = trounds;
+        }
+      }
+      // ---- early exit (robust_estimator.py:163-164)
+      if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
+      // ---- tau_i = (C W^1/2 u)_i^2 / lambda
+      double t0, t1;
+      {
+        const double z0 = sw0 * u0, z1 = sw1 * u1;
+        wsym::put_operand(zd, z0, z1);
+        wsym::matvec<WKV>(P, cl, zd, tb, z0, z1, t0, t1);
+      }
+      const double ti0 = t0 * t0 / lam, ti1 = t1 * t1 / lam;
+      // filterL2 (:166-172): c *= 1 - tau / tau_max, the argmax (first index)
+      // removed, c /= |c|_1
+      double tmax = 0.0;
+      {
+        const double v0 = ai0 ? ti0 : -__builtin_inf(), v1 = ai1 ? ti1 : -__builtin_inf();
+        const bool take1 = v1 > v0;
+        const int p = wave_argmax_first(take1 ? v1 : v0, take1 ? r1 : r0, &tmax);
+        const double cn0 = (ai0 && r0 != p) ? ci0 * (1.0 - ti0 / tmax) : 0.0;
+        const double cn1 = (ai1 && r1 != p) ? ci1 * (1.0 - ti1 / tmax) : 0.0;
+        const double l1 = wave_sum(fabs(cn0) + fabs(cn1));
+        ci0 = cn0 / l1;
+        ci1 = cn1 / l1;
+        if (r0 == p) ai0 = false;
+        if (r1 == p) ai1 = false;
+        if (tr != nullptr && lane == 0) tr[1 + it] = p;
+      }
+      done = it + 1;
+    }
+
+    if (fallback) {
+      if (lane == 0) {
+        const int k = atomicAdd(A.fb_count, 1);
+        A.fb_list[k] = ch;
+      }
+      continue;
+    }
+    {
+      const double c0 = ai0 ? ci0 : 0.0, c1 = ai1 ? ci1 : 0.0;
+      reinterpret_cast<double2*>(A.c + static_cast<size_t>(ch) * FNP)[lane] = double2{c0, c1};
+      reinterpret_cast<int2*>(A.act + static_cast<size_t>(ch) * FNP)[lane] = int2{ai0 ? 1 : 0, ai1 ? 1 : 0};
+      if (tr != nullptr) {
+        tr[1 + FNP + r0] = ai0 ? 1 : 0;
+        tr[1 + FNP + r1] = ai1 ? 1 : 0;
+        if (lane == 0) tr[0] = done;
+      }
+      // np.average's scale: numpy's pairwise sum of the kept weights in client order
+      double* cv = zd;             // [FNP] weights
+      double* kf = tb;             // [FNP] kept flags
+      wsym::lds_order();
+      reinterpret_cast<double2*>(cv)[lane] = double2{c0, c1};
+      reinterpret_cast<double2*>(kf)[lane] = double2{ai0 ? 1.0 : 0.0, ai1 ? 1.0 : 0.0};
+      wsym::lds_order();
+      if (lane == 0) {
+        double* kept = tb + FNP;   // [FNP]
+        int q2 = 0;
+        for (int i = 0; i < n; ++i)
+          if (kf[i] != 0.0) kept[q2++] = cv[i];
+        A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
+      }
+      wsym::lds_order();
+    }
+  }
+}
+
+size_t wave_solve_lds() { return kWaveLds; }
+int wave_solve_grid() { return kWaveGrid; }
+
+int launch_wave_solve(bool dbg, const SolveArgs& sa, int grid, hipStream_t s) {
+  const void* k = dbg ? reinterpret_cast<const void*>(&wave_solve_kernel<0, true>)
+                      : reinterpret_cast<const void*>(&wave_solve_kernel<0, false>);
+  SRA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kWaveLds)));
+  if (dbg) hipLaunchKernelGGL((wave_solve_kernel<0, true>), dim3(grid), dim3(64), kWaveLds, s, sa);
+  else hipLaunchKernelGGL((wave_solve_kernel<0, false>), dim3(grid), dim3(64), kWaveLds, s, sa);
+  return launch_status("wave_solve_kernel");
+}
+
+}  // namespace sra
