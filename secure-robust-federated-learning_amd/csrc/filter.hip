@@ -2703,7 +2703,7 @@ size_t filter_workspace_bytes(int n, int64_t d, int itv) {
   const int64_t nchunks = cdiv(d, itv);
   const int64_t b = nchunks < kBatch ? nchunks : kBatch;
   const int64_t grid = b < kLanczosGrid ? b : kLanczosGrid;
-  return static_cast<size_t>(b) * kChunkWsBytes + static_cast<size_t>(grid) * MMAX * FNP * sizeof(double) + 528;
+  return static_cast<size_t>(b) * kChunkWsBytes + static_cast<size_t>(grid) * (MMAX + 1) * FNP * sizeof(double) + 528;
 }
 
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
@@ -2726,7 +2726,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   double* cws = Gws + static_cast<size_t>(bmax) * FNP * FNP;
   double* mws = cws + static_cast<size_t>(bmax) * FNP;
   double* Vws = mws + static_cast<size_t>(bmax) * kMisc;
-  int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(lgrid_max) * MMAX * FNP);
+  int* aws = reinterpret_cast<int*>(Vws + static_cast<size_t>(lgrid_max) * (MMAX + 1) * FNP);   // wave_solve_kernel: MMAX + 1 basis slots per wave
   int* fbl = aws + static_cast<size_t>(bmax) * FNP;
   int* fbc = fbl + bmax;   // [0] listed chunks, [1] ghost after the retry, [2] out of steps, [3] retries,
                            // [4] the solver's chunk queue

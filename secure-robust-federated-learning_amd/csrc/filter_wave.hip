@@ -46,7 +46,7 @@
 
 namespace sra {
 
-constexpr int WKV = 40;                       // C's diagonals in VGPRs (tools/ubench/wave_step.hip: 32 / 40 / 48)
+constexpr int WKV = 36;                       // C's diagonals in VGPRs (the rest in LDS: four waves per CU fill it)
 constexpr int WKL = wsym::NK - WKV;           // ... in LDS
 constexpr int kExStride = 72;                 // check: exponents per block of 4 chain steps, per chain
 constexpr int kWScr = 4 * MMAX + 2 * kExStride;   // operand (256) + group shifts (384) | check scratch
@@ -407,9 +407,8 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
   const int lane = threadIdx.x;
   const int r0 = 2 * lane, r1 = r0 + 1;
   const int n = A.n;
-  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * MMAX * FNP;
+  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * (MMAX + 1) * FNP;
   if (lane < 32) trw[2 * MMAX + lane] = 0.0;   // prefetch padding of the T record
-  if (lane == 0) trw[1] = 0.0;                   // beta^2_{-1}: multiplies a zero in the check's forward chain
 
   for (;;) {
     int ch = lane == 0 ? atomicAdd(A.fb_count + 4, 1) : 0;
@@ -473,7 +472,6 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       for (int attempt = 0; attempt < 3 && !converged; ++attempt) {
         const bool reorth = attempt == 2;
         double rt0 = sw0 > 0.0 ? sw0 * hh0 : 0.0, rt1 = sw1 > 0.0 ? sw1 * hh1 : 0.0;
-        double nrm2 = wave_sum(rt0 * rt0 + rt1 * rt1);
         double qp0 = 0.0, qp1 = 0.0, theta_lb = -1e300, hint = -1.0;
         double res_best = 1e300, lam_best = 0.0;
         tscale = 0.0;
@@ -484,71 +482,13 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         int m_a = -1, m_last = 4, m_pre = 4;
         double res_a = 0.0;
         bool ghost = false;
+        // Step j: y = M r~_j (r~_j = beta_j q_j, deferred normalisation), and
+        // beta_j^2 = |r~_j|^2, its square root and reciprocal in the same basic
+        // block (the reduction overlaps the matvec), then alpha_j and r~_{j+1};
+        // the check of T_j (m = j, residual beta_j |z_{j-1}|) runs after that,
+        // so no branch separates the matvec from the reduction, and a check
+        // that accepts has spent one step for nothing.
         for (int j = 0;; ++j) {
-          const double bet = sqrt(nrm2);
-          if (j > 0) {
-            trw[2 * j + 1] = nrm2;   // every lane stores the same value: no exec-mask branch
-            tscale = fmax(tscale, bet);
-            const bool breakdown = !(bet > 1e-14 * tscale);
-            if (breakdown || j == MMAX || j >= next_check) {
-              const int m = j;
-              wsym::lds_order();   // lane 0's T record entries
-              ++nchecks;
-              const long long tc0 = dbg ? clock64() : 0;
-              double lm, zl;
-              int rounds = 0;
-              const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
-              wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, scr, &lm, &zl, &rounds);
-              if (dbg) {
-                tcheck += clock64() - tc0;
-                trounds += rounds;
-              }
-              const double res = fabs(bet * zl);
-              hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
-              theta_lb = lm;
-              if (res <= kAccept * fabs(lm) || breakdown) {
-                converged = true;
-                m_conv = m;
-                lam = lm;
-                resid = res;
-                zbest = zcur;
-                break;
-              }
-              if (res < res_best) {
-                m_pre = m_last;
-                res_best = res;
-                lam_best = lm;
-                zbest = zcur;
-                zcur ^= 1;
-              }
-              ghost = !reorth && res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
-              const bool out_of_steps = j == MMAX;
-              if (ghost || out_of_steps) {
-                if (lane == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
-                if (!ghost && attempt < 2) {   // out of steps: straight on to the re-orthogonalising attempt
-                  ghost = true;
-                  attempt = 1;
-                }
-                m_retry = m_pre;
-                break;
-              }
-              int adv = 4;
-              double rate = rate_hint;
-              if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
-              if (rate < 0.0 && res > 0.0) {
-                const double need = log(kAccept * fabs(lm) / res) / rate;
-                adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
-              }
-              m_a = m;
-              res_a = res;
-              m_last = m;
-              next_check = m + adv;
-            }
-            gfin_hi = fmax(gfin_hi, a_last + b_prev + bet);
-            gfin_lo = fmin(gfin_lo, a_last - b_prev - bet);
-            b_prev = bet;
-          }
-          // y = M r~ (r~ = beta q_j), alpha_j = q_j . M q_j
           const long long ts0 = dbg ? clock64() : 0;
           double y0, y1;
           {
@@ -556,9 +496,22 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
             wsym::put_operand(zd, z0, z1);
             wsym::matvec<WKV>(P, cl, zd, tb, z0, z1, y0, y1);
           }
+          const double nrm2 = wave_sum(rt0 * rt0 + rt1 * rt1);
+          const double bet = sqrt(nrm2);
+          const double ib = 1.0 / bet;
           const long long ts1 = dbg ? clock64() : 0;
           if (dbg) tmv += ts1 - ts0;
-          const double ib = 1.0 / bet;
+          trw[2 * j + 1] = nrm2;   // every lane stores the same value (no exec-mask branch); T[1] is never used
+          tscale = j > 0 ? fmax(tscale, bet) : tscale;
+          const bool breakdown = j > 0 && !(bet > 1e-14 * tscale);
+          const bool do_check = j > 0 && (breakdown || j == MMAX || j >= next_check);
+          // Gershgorin bounds of T_j: rows 0 .. j-2 final, row j-1 with beta_{j-1} and beta_j
+          const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
+          gfin_hi = j > 0 ? fmax(gfin_hi, a_last + b_prev + bet) : gfin_hi;
+          gfin_lo = j > 0 ? fmin(gfin_lo, a_last - b_prev - bet) : gfin_lo;
+          b_prev = j > 0 ? bet : b_prev;
+          // alpha_j = q_j . M q_j (the basis has MMAX + 1 slots: q_MMAX of the
+          // step whose check ends the attempt is stored and never read)
           const double q0 = rt0 * ib, q1 = rt1 * ib;
           reinterpret_cast<double2*>(Vb + j * FNP)[lane] = double2{q0, q1};
           const double mq0 = sw0 * y0 * ib, mq1 = sw1 * y1 * ib;
@@ -603,14 +556,66 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
             }
           }
           trw[2 * j] = aj;   // every lane: no exec-mask branch
+          if (dbg) tstep += clock64() - ts1;
+          if (do_check) {
+            const int m = j;
+            wsym::lds_order();   // the T record
+            ++nchecks;
+            const long long tc0 = dbg ? clock64() : 0;
+            double lm, zl;
+            int rounds = 0;
+            wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, scr, &lm, &zl, &rounds);
+            if (dbg) {
+              tcheck += clock64() - tc0;
+              trounds += rounds;
+            }
+            const double res = fabs(bet * zl);
+            hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
+            theta_lb = lm;
+            if (res <= kAccept * fabs(lm) || breakdown) {
+              converged = true;
+              m_conv = m;
+              lam = lm;
+              resid = res;
+              zbest = zcur;
+              break;
+            }
+            if (res < res_best) {
+              m_pre = m_last;
+              res_best = res;
+              lam_best = lm;
+              zbest = zcur;
+              zcur ^= 1;
+            }
+            ghost = !reorth && res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
+            const bool out_of_steps = j == MMAX;
+            if (ghost || out_of_steps) {
+              if (lane == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
+              if (!ghost && attempt < 2) {   // out of steps: straight on to the re-orthogonalising attempt
+                ghost = true;
+                attempt = 1;
+              }
+              m_retry = m_pre;
+              break;
+            }
+            int adv = 4;
+            double rate = rate_hint;
+            if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
+            if (rate < 0.0 && res > 0.0) {
+              const double need = log(kAccept * fabs(lm) / res) / rate;
+              adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
+            }
+            m_a = m;
+            res_a = res;
+            m_last = m;
+            next_check = m + adv;
+          }
           a_last = aj;
           tscale = fmax(tscale, fabs(aj));
           qp0 = q0;
           qp1 = q1;
           rt0 = n0;
           rt1 = n1;
-          nrm2 = wave_sum(n0 * n0 + n1 * n1);
-          if (dbg) tstep += clock64() - ts1;
         }
         if (!ghost) break;
       }

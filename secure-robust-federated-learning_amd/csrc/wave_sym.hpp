@@ -120,6 +120,9 @@ __device__ __forceinline__ void matvec(const Packed<KV>& P, const double* __rest
   const double2* xp = reinterpret_cast<const double2*>(zd) + lane;   // xp[j] = (z_{2l+2j}, z_{2l+2j+1})
   double a[4][2];
   double h[4][2];
+  // operand window of each group: xw[g][0] = X_j, xw[g][1] = X_{j+1} for the
+  // group's current diagonal k (j = k / 2); every X is one aligned b128 read
+  double2 xw[4][2];
   {
     const double2 c0 = diag<KV, 0>(P, cl, lane);
     a[0][0] = c0.x * z0;
@@ -132,17 +135,24 @@ __device__ __forceinline__ void matvec(const Packed<KV>& P, const double* __rest
     sfor<4>([&](auto Gi) {
       constexpr int g = decltype(Gi)::value;
       constexpr int k = 16 * g + 16 - r;
-      const double2 c = diag<KV, k>(P, cl, lane);
-      // ---- a part: j = k / 2
       constexpr int j = k / 2;
-      const double2 X = xp[j];
+      const double2 c = diag<KV, k>(P, cl, lane);
+      // ---- a part: k even uses X_j; k odd uses X_j.y and X_{j+1}.x.  Going
+      // down, an odd k loads X_j (X_{j+1} is the previous round's), the even
+      // k = 2j that follows reuses it; a group's first k loads what it needs.
+      if constexpr (r == 0) {
+        xw[g][0] = xp[j];
+        if constexpr (k & 1) xw[g][1] = xp[j + 1];
+      } else if constexpr (k & 1) {
+        xw[g][1] = xw[g][0];
+        xw[g][0] = xp[j];
+      }
       if constexpr ((k & 1) == 0) {
-        a[g][0] = fma(c.x, X.x, a[g][0]);
-        a[g][1] = fma(c.y, X.y, a[g][1]);
+        a[g][0] = fma(c.x, xw[g][0].x, a[g][0]);
+        a[g][1] = fma(c.y, xw[g][0].y, a[g][1]);
       } else {
-        const double2 X1 = xp[j + 1];
-        a[g][0] = fma(c.x, X.y, a[g][0]);
-        a[g][1] = fma(c.y, X1.x, a[g][1]);
+        a[g][0] = fma(c.x, xw[g][0].y, a[g][0]);
+        a[g][1] = fma(c.y, xw[g][1].x, a[g][1]);
       }
       // ---- b part (k <= 63), Horner from the group's top diagonal down
       if constexpr (k <= 63) {
