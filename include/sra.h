@@ -281,6 +281,23 @@ int sra_filter_debug_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int3
                          double eps, double sigma, double expansion, double* out, int32_t* status, double* dbg,
                          void* ws, size_t ws_bytes, void* stream);
 
+/* Workspace for sra_mom_filter_f32, in bytes (nbuckets <= 128). */
+int sra_mom_filter_workspace_bytes(int64_t nbuckets, int64_t d, int32_t itv, size_t* bytes);
+
+/* The median-of-means forms in one call: mode 0 robust_estimator.mom_filterL2
+ * (src/robust_estimator.py:210-218), mode 1 mom_ex_noregret (:135-142).  X
+ * holds the n clients; filtered row r is the np.mean of clients
+ * [r * bucket_size, min((r + 1) * bucket_size, n)), formed inside the chunk-Gram
+ * loads (a sequential fp32 sum over the bucket's clients / their count, the
+ * bits sra_bucket_mean_f32 writes) -- the bucket matrix is never written as a
+ * whole; each batch's bucket rows go to the workspace for the chunk means.
+ * Results equal sra_bucket_mean_f32 followed by sra_filter_f32 bit for bit.
+ * nbuckets <= 128 (SRA_ERR_UNSUPPORTED above: run the two calls instead); an
+ * empty trailing bucket -> SRA_ERR_EMPTY_BUCKET (the reference's ValueError). */
+int sra_mom_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
+                       int32_t bucket_size, int32_t nbuckets, double eps, double sigma, double expansion,
+                       double* out, int32_t* status, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Cross-layer-norm clipping (k7): the stateful inline aggregators           */
 /* iclr2022_bucketing (src/simulate.py:335-366) and icml2021_history (:367-388) */

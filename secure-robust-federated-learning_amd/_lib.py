@@ -90,6 +90,9 @@ _SIGS = {
                              _ptr],
     "sra_filter_debug_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _dbl, _dbl, _dbl, _ptr, _ptr, _ptr, _ptr, _sz,
                              _ptr],
+    "sra_mom_filter_workspace_bytes": [_i64, _i64, _i32, ctypes.POINTER(_sz)],
+    "sra_mom_filter_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _dbl, _dbl, _dbl, _ptr, _ptr, _ptr, _sz,
+                           _ptr],
     "sra_window_mean_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _i32, _ptr, _i64, _ptr],
     "sra_window_mean_f64": [_ptr, _i64, _i64, _i64, _i32, _i32, _i32, _ptr, _i64, _ptr],
     "sra_clip_workspace_bytes": [_i64, ctypes.POINTER(_i64), _i32, ctypes.POINTER(_sz)],

@@ -62,6 +62,15 @@ struct GramArgs {
   int64_t chunk0;   // first chunk of the batch
   int nb;           // chunks in the batch
   double* G;        // [nb][FNP][FNP]
+  // MoM filters (round 5): bs > 0 -> X holds nsrc clients and row r of the
+  // filtered matrix is the mean of clients [r bs, min((r+1) bs, nsrc)),
+  // formed in the stage loads with bucket_mean_kernel's arithmetic (np.mean:
+  // a sequential fp32 sum / the count) and written to Bout[r][col - chunk0 itv]
+  // for the chunk-mean pass -- the separate bucket pass is gone
+  int bs;
+  int nsrc;
+  float* Bout;
+  int64_t ldb;
 };
 
 constexpr int ftile_i(int t) {
@@ -98,7 +107,18 @@ __device__ __forceinline__ void gram_tiles(const GramArgs& A, int64_t k0, int k,
     for (int e = tid; e < FNP * FST; e += 256) {
       const int r = e / FST, cc = e - (e / FST) * FST;
       float v = 0.f;
-      if (r < n && s0 + cc < k) v = A.X[static_cast<int64_t>(r) * A.ldx + k0 + s0 + cc];
+      if (r < n && s0 + cc < k) {
+        const int64_t col = k0 + s0 + cc;
+        if (A.bs > 0) {
+          const int lo = r * A.bs, hi = lo + A.bs < A.nsrc ? lo + A.bs : A.nsrc;
+          float acc = 0.f;
+          for (int i = lo; i < hi; ++i) acc += A.X[static_cast<int64_t>(i) * A.ldx + col];
+          v = acc / static_cast<float>(hi - lo);
+          A.Bout[static_cast<int64_t>(r) * A.ldb + (col - A.chunk0 * A.itv)] = v;
+        } else {
+          v = A.X[static_cast<int64_t>(r) * A.ldx + col];
+        }
+      }
       stage[r * FROW + cc] = v;
     }
     __syncthreads();
@@ -2017,7 +2037,7 @@ __global__ void list_all_kernel(int* list, int* count, int nb) {
 // chunk_mean_kernel: the weighted mean of every coordinate of the batch
 // ============================================================================
 __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
-                                                         int itv, int64_t chunk0, int nb,
+                                                         int64_t jx0, int itv, int64_t chunk0, int nb,
                                                          const double* __restrict__ c, const int* __restrict__ act,
                                                          const double* __restrict__ misc, double* __restrict__ out,
                                                          int cs, int unw) {
@@ -2036,7 +2056,7 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
     int cnt = 0;
     for (int i = 0; i < n; ++i)
       if (ab[i]) {
-        s32 += X[static_cast<int64_t>(i) * ldx + j];
+        s32 += X[static_cast<int64_t>(i) * ldx + (j - jx0)];
         ++cnt;
       }
     out[j] = static_cast<double>(s32 / static_cast<float>(cnt));
@@ -2044,7 +2064,7 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
   }
   double s = 0.0;
   for (int i = 0; i < n; ++i)
-    if (ab[i]) s += static_cast<double>(X[static_cast<int64_t>(i) * ldx + j]) * cb[i];
+    if (ab[i]) s += static_cast<double>(X[static_cast<int64_t>(i) * ldx + (j - jx0)]) * cb[i];
   out[j] = s / misc[static_cast<size_t>(b) * kMisc];
 }
 
@@ -2690,31 +2710,35 @@ int launch_filter_big(int mode, const float* X, int n, int64_t d, int64_t ldx, i
     }
     rc = launch_status("filter_big_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws, aws,
-                       mws, out, NB, mode);
+    hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, int64_t(0), itv, c0,
+                       nb, cws, aws, mws, out, NB, mode);
     rc = launch_status("chunk_mean_kernel");
     if (rc) return rc;
   }
   return SRA_OK;
 }
 
-size_t filter_workspace_bytes(int n, int64_t d, int itv) {
+// bucketed: the MoM form's bucket rows of one batch (n x batch columns fp32)
+size_t filter_workspace_bytes(int n, int64_t d, int itv, bool bucketed) {
   if (n > FNP) return filter_big_workspace_bytes(n, d, itv);
   const int64_t nchunks = cdiv(d, itv);
   const int64_t b = nchunks < kBatch ? nchunks : kBatch;
   const int64_t grid = b < kLanczosGrid ? b : kLanczosGrid;
-  return static_cast<size_t>(b) * kChunkWsBytes + static_cast<size_t>(grid) * (MMAX + 1) * FNP * sizeof(double) + 528;
+  return static_cast<size_t>(b) * kChunkWsBytes + static_cast<size_t>(grid) * (MMAX + 1) * FNP * sizeof(double) + 528 +
+         (bucketed ? static_cast<size_t>(n) * b * itv * sizeof(float) + 256 : 0);
 }
 
+// bs > 0: the MoM forms -- X holds nsrc clients, n = the bucket count (<= FNP)
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
                   double expansion, double* out, int* status, double* dbg, int* trace, void* ws, size_t ws_bytes,
-                  hipStream_t s) {
+                  hipStream_t s, int bs = 0, int nsrc = 0) {
   SRA_REQUIRE(n >= 1 && n <= NBIG2, SRA_ERR_UNSUPPORTED, "spectral filters support 1 <= N <= %d (got %d)", NBIG2, n);
   SRA_REQUIRE(itv >= 1, SRA_ERR_ARG, "itv must be >= 1");
   const int64_t nchunks = cdiv(d, itv);
   SRA_REQUIRE(nchunks < (int64_t(1) << 31), SRA_ERR_ARG, "too many chunks");
-  SRA_REQUIRE(ws != nullptr && ws_bytes >= filter_workspace_bytes(n, d, itv), SRA_ERR_WORKSPACE,
-              "filter workspace too small: need %zu bytes", filter_workspace_bytes(n, d, itv));
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= filter_workspace_bytes(n, d, itv, bs > 0), SRA_ERR_WORKSPACE,
+              "filter workspace too small: need %zu bytes", filter_workspace_bytes(n, d, itv, bs > 0));
+  SRA_REQUIRE(bs == 0 || n <= FNP, SRA_ERR_UNSUPPORTED, "fused MoM filters take <= %d buckets (got %d)", FNP, n);
   if (n > FNP) {
     SRA_REQUIRE(dbg == nullptr, SRA_ERR_UNSUPPORTED, "filter debug records support N <= %d (got %d)", FNP, n);
     return launch_filter_big(mode, X, n, d, ldx, itv, eps, sigma, expansion, out, status, trace, ws, s);
@@ -2730,6 +2754,9 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   int* fbl = aws + static_cast<size_t>(bmax) * FNP;
   int* fbc = fbl + bmax;   // [0] listed chunks, [1] ghost after the retry, [2] out of steps, [3] retries,
                            // [4] the solver's chunk queue
+  const int64_t ldb = bmax * itv;   // bucket rows of a batch (MoM forms)
+  float* Bws = bs > 0 ? reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(fbc + 8) + 255) & ~uintptr_t(255))
+                      : nullptr;
   const void* solve = mode == 0 ? (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<0, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<0, false>))
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
@@ -2744,7 +2771,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   // fixtures missed rtol 1e-5 (DESIGN k6)
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
-    GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws};
+    GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws, bs, nsrc, Bws, ldb};
     hipLaunchKernelGGL(chunk_gram_kernel, dim3(nb), dim3(256), 0, s, ga);
     int rc = launch_status("chunk_gram_kernel");
     if (rc) return rc;
@@ -2756,9 +2783,11 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       rc = launch_status("noregret_pre_kernel");
       if (rc) return rc;
     }
-    // check schedule of the plain solver: first check 8 steps before the
-    // previous iteration's step count (-4: 186.5 ms, 0: 353 ms at C4, DESIGN k6)
-    constexpr int first_off = -8;
+    // check schedule of the one-wave solver: first check 12 steps before the
+    // previous iteration's step count -- a check (~25k cycles) costs ~6 steps,
+    // a late first check a ghost and a dense retry (C4 filterL2: -8 106.0 ms,
+    // -12 91.0, -16 92.4, -20 93.5; 0 221, DESIGN k6)
+    constexpr int first_off = -12;
     SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
                  trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr, first_off,
                  kMaxAdvance, 0};
@@ -2790,8 +2819,9 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
       SRA_HIP(hipMemcpyAsync(dbg + FNP * FNP + 255 * kDbgRec + kDbgRec - 3, fbc, 6 * sizeof(int), hipMemcpyDeviceToDevice, s));
     const int64_t jend = (c0 + nb) * static_cast<int64_t>(itv);
     const int64_t ncols = (jend < d ? jend : d) - c0 * static_cast<int64_t>(itv);
-    hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, X, n, d, ldx, itv, c0, nb, cws,
-                       aws, mws, out, FNP, mode);
+    // the chunk means read the filtered rows: X itself, or the batch's bucket rows
+    hipLaunchKernelGGL(chunk_mean_kernel, dim3(cdiv(ncols, 256)), dim3(256), 0, s, bs > 0 ? Bws : X, n, d,
+                       bs > 0 ? ldb : ldx, bs > 0 ? c0 * itv : int64_t(0), itv, c0, nb, cws, aws, mws, out, FNP, mode);
     rc = launch_status("chunk_mean_kernel");
     if (rc) return rc;
   }
@@ -2819,8 +2849,30 @@ static int filter_checks(const float* X, int64_t n, int64_t d, int64_t ldx, int3
 extern "C" int sra_filter_workspace_bytes(int64_t n, int64_t d, int32_t itv, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
   SRA_REQUIRE(n >= 1 && d >= 1 && itv >= 1, SRA_ERR_SHAPE, "bad shape");
-  *bytes = sra::filter_workspace_bytes(static_cast<int>(n), d, itv);
+  *bytes = sra::filter_workspace_bytes(static_cast<int>(n), d, itv, false);
   return SRA_OK;
+}
+
+extern "C" int sra_mom_filter_workspace_bytes(int64_t nbuckets, int64_t d, int32_t itv, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(nbuckets >= 1 && nbuckets <= sra::FNP && d >= 1 && itv >= 1, SRA_ERR_SHAPE, "bad shape");
+  *bytes = sra::filter_workspace_bytes(static_cast<int>(nbuckets), d, itv, true);
+  return SRA_OK;
+}
+
+extern "C" int sra_mom_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,
+                                  int32_t bucket_size, int32_t nbuckets, double eps, double sigma, double expansion,
+                                  double* out, int32_t* status, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(n >= 1, SRA_ERR_SHAPE, "bad shape");
+  SRA_REQUIRE(bucket_size >= 1 && nbuckets >= 1 && nbuckets <= sra::FNP, SRA_ERR_UNSUPPORTED,
+              "fused MoM filters take 1 <= nbuckets <= %d (got %d)", sra::FNP, nbuckets);
+  SRA_REQUIRE(static_cast<int64_t>(nbuckets - 1) * bucket_size < n, SRA_ERR_EMPTY_BUCKET,
+              "bucket %d of size %d is empty for N=%lld (the reference's np.mean of an empty slice)",
+              (int)((n + bucket_size - 1) / bucket_size), bucket_size, (long long)n);
+  const int rc = sra::filter_checks(X, nbuckets, d, ldx, mode, eps, out, status);
+  if (rc) return rc;
+  return sra::launch_filter(mode, X, nbuckets, d, ldx, itv, eps, sigma, expansion, out, status, nullptr, nullptr, ws,
+                            ws_bytes, static_cast<hipStream_t>(stream), bucket_size, static_cast<int>(n));
 }
 
 extern "C" int sra_filter_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t mode, int32_t itv,

@@ -56,14 +56,47 @@ constexpr size_t kWaveLds = sizeof(double) * (static_cast<size_t>(WKL) * FNP + k
 static_assert(4 * kWaveLds <= 163840, "four one-wave solvers must fit one CU's LDS");
 constexpr int kWaveGrid = 1024;               // 4 waves per CU x 256 CUs; each owns a basis slot
 
+// The pairs T2[q] = (alpha_q, beta^2 of (q-1, q)) for q = 1 .. m-1 into f, g()
+// after every fourth: the next block's four LDS reads are issued before the
+// current block's steps, so a serial chain (~30 cycles a step) does not wait
+// on LDS latency (reads reach T2[m + 6], inside the record's padding).
+template <typename F, typename G>
+__device__ __forceinline__ void tstream(const double2* T2, int m, F&& f, G&& g) {
+  double2 c0 = T2[1], c1 = T2[2], c2 = T2[3], c3 = T2[4];
+  int q = 1;
+  for (; q + 4 <= m; q += 4) {
+    const double2 n0 = T2[q + 4], n1 = T2[q + 5], n2 = T2[q + 6], n3 = T2[q + 7];
+    f(c0);
+    f(c1);
+    f(c2);
+    f(c3);
+    g();
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+  }
+  if (q < m) f(c0);
+  if (q + 1 < m) f(c1);
+  if (q + 2 < m) f(c2);
+}
+
 // ---- the check: top Ritz pair of T_m in one wave ---------------------------
 // T: LDS record, T[2q] = alpha_q, T[2q+1] = beta^2 of (q-1, q) (T[1] = 0).
 // Returns theta (2-ulp bracket midpoint), the last component of the
 // normalised eigenvector (the residual is beta_m |z_{m-1}|), and writes z[0, m).
 __device__ __forceinline__ void wave_check(const double* T, int m, double theta_lb, double hint, double glo,
                                            double ghi, double* z, double* scr, double* theta_out,
-                                           double* zlast_out, int* rounds_out) {
+                                           double* zlast_out, int* rounds_out, long long* ph = nullptr) {
   m = __builtin_amdgcn_readfirstlane(m);
+  long long tp = ph ? clock64() : 0;
+  auto stamp = [&](int i) {   // debug builds: cycles per check phase
+    if (ph) {
+      const long long t = clock64();
+      ph[i] += t - tp;
+      tp = t;
+    }
+  };
   const int lane = threadIdx.x & 63;
   double* gq = scr;                  // [MMAX] g | [MMAX] Q  (forward chain)
   double* hr = scr + 2 * MMAX;       // [MMAX] h | [MMAX] R  (backward chain)
@@ -86,80 +119,21 @@ __device__ __forceinline__ void wave_check(const double* T, int m, double theta_
       p2 = p1;
       p1 = pk;
     };
-    double2 c0 = T2[1], c1 = T2[2];
-    int q = 1;
-    for (; q + 4 <= m; q += 4) {
-      const double2 c2 = T2[q + 2], c3 = T2[q + 3];
-      step(c0);
-      step(c1);
-      c0 = T2[q + 4];
-      c1 = T2[q + 5];
-      step(c2);
-      step(c3);
+    tstream(T2, m, step, [&]() __attribute__((always_inline)) {
       const int e = __builtin_amdgcn_frexp_exp(p1);
       p1 = __builtin_amdgcn_ldexp(p1, -e);
       p2 = __builtin_amdgcn_ldexp(p2, -e);
-    }
-    if (q < m) step(c0);
-    if (q + 1 < m) step(c1);
-    if (q + 2 < m) step(T2[q + 2]);
+    });
     return static_cast<int>(cnt);
   };
-  // cold start: Laguerre from the Gershgorin upper bound (fast_check)
-  bool laguerre = false;
+  // one multisection round: 64 Sturm points (one per lane) of the given kind
+  // in [lo, hi]; returns true when the bracket is at two ulps (or stalled).
+  // kind 0 uniform, 1 geometric above lo up to lo + 4 hint (hinted checks),
+  // 2 geometric above lo over the whole bracket (cold), 3 the Laguerre bracket
+  // with both ends included (verifies it; false + reset when it misses)
   const double lo0 = lo, hi0 = hi;
-  if (!hinted && m > 2) {
-    double x = hi;
-    for (int itl = 0; itl < 16; ++itl) {
-      double p0 = 1.0, p1 = x - a0, d0 = 0.0, d1 = 1.0, e0 = 0.0, e1 = 0.0;
-      auto lstep = [&](double2 t) __attribute__((always_inline)) {
-        const double c = x - t.x;
-        const double pn = fma(c, p1, -(t.y * p0));
-        const double dn = fma(c, d1, p1 - t.y * d0);
-        const double en = fma(c, e1, 2.0 * d1 - t.y * e0);
-        p0 = p1; p1 = pn;
-        d0 = d1; d1 = dn;
-        e0 = e1; e1 = en;
-      };
-      double2 c0 = T2[1], c1 = T2[2];
-      int q = 1;
-      for (; q + 4 <= m; q += 4) {
-        const double2 c2 = T2[q + 2], c3 = T2[q + 3];
-        lstep(c0);
-        lstep(c1);
-        c0 = T2[q + 4];
-        c1 = T2[q + 5];
-        lstep(c2);
-        lstep(c3);
-        const int e = __builtin_amdgcn_frexp_exp(fmax(fabs(p1), fabs(d1)));
-        p0 = __builtin_amdgcn_ldexp(p0, -e); p1 = __builtin_amdgcn_ldexp(p1, -e);
-        d0 = __builtin_amdgcn_ldexp(d0, -e); d1 = __builtin_amdgcn_ldexp(d1, -e);
-        e0 = __builtin_amdgcn_ldexp(e0, -e); e1 = __builtin_amdgcn_ldexp(e1, -e);
-      }
-      if (q < m) lstep(c0);
-      if (q + 1 < m) lstep(c1);
-      if (q + 2 < m) lstep(T2[q + 2]);
-      if (!(p1 != 0.0)) break;
-      const double G = d1 / p1, H = G * G - e1 / p1;
-      const double nn = static_cast<double>(m);
-      const double den = G + sqrt(fmax((nn - 1.0) * (nn * H - G * G), 0.0));
-      const double xn = x - nn / den;
-      if (!(xn < x) || !(xn >= lo0)) break;
-      const bool fin = x - xn <= 4e-16 * fabs(x);
-      x = xn;
-      if (fin) break;
-    }
-    const double u = 64.0 * 2.2204460492503131e-16 * fabs(x);
-    if (x - u > lo0 && x + u < hi0) {
-      lo = x - u;
-      hi = x + u;
-      laguerre = true;
-    }
-  }
-  // multisection: 64 Sturm points per round, one per lane
-  int round = 0;
-  for (; round < 48; ++round) {
-    const int kind = round == 0 ? (laguerre ? 3 : (hinted && hg < hi ? 1 : 2)) : 0;
+  bool laguerre = false;
+  auto mround = [&](int kind) -> bool {
     const double rlo = lo, rhi = hi;
     auto point = [&](int p) -> double {
       if (kind == 1) return p < 63 ? rlo + (hg - rlo) * ((p + 1) * (1.0 / 63.0)) : rhi;
@@ -169,20 +143,80 @@ __device__ __forceinline__ void wave_check(const double* T, int m, double theta_
     };
     const unsigned long long ok = __builtin_amdgcn_ballot_w64(count(point(lane)) >= m);
     const int first = ok ? __builtin_ctzll(ok) : 64;
-    if (kind == 3 && (first == 0 || first == 64)) {
+    if (kind == 3 && (first == 0 || first == 64)) {   // not inside the Laguerre bracket
       lo = lo0;
       hi = hi0;
       laguerre = false;
-      continue;
+      return false;
     }
     const double xf = first < 64 ? point(first) : rhi;
     const double xb = first > 0 ? point(first - 1) : rlo;
     const bool stalled = xb == lo && xf == hi;
     lo = xb;
     hi = xf;
-    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
+    return stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi));
+  };
+  int round = 0;
+  bool done = false;
+  // cold start: two multisection rounds (geometric above the lower bound, then
+  // uniform) bracket the top eigenvalue to ~1e-4 of the Gershgorin range, then
+  // Laguerre from the bracket's top (above the spectrum: it decreases
+  // monotonically to the top eigenvalue, cubically this close), then one
+  // round over +-64 ulps verifies it
+  if (!hinted && m > 2) {
+    done = mround(2);
+    ++round;
+    if (!done) {
+      done = mround(0);
+      ++round;
+    }
+    if (!done) {
+      const double llo = lo;
+      double x = hi;
+      for (int itl = 0; itl < 16; ++itl) {
+        double p0 = 1.0, p1 = x - a0, d0 = 0.0, d1 = 1.0, e0 = 0.0, e1 = 0.0;
+        auto lstep = [&](double2 t) __attribute__((always_inline)) {
+          const double c = x - t.x;
+          const double pn = fma(c, p1, -(t.y * p0));
+          const double dn = fma(c, d1, p1 - t.y * d0);
+          const double en = fma(c, e1, 2.0 * d1 - t.y * e0);
+          p0 = p1; p1 = pn;
+          d0 = d1; d1 = dn;
+          e0 = e1; e1 = en;
+        };
+        tstream(T2, m, lstep, [&]() __attribute__((always_inline)) {
+          const int e = __builtin_amdgcn_frexp_exp(fmax(fabs(p1), fabs(d1)));
+          p0 = __builtin_amdgcn_ldexp(p0, -e); p1 = __builtin_amdgcn_ldexp(p1, -e);
+          d0 = __builtin_amdgcn_ldexp(d0, -e); d1 = __builtin_amdgcn_ldexp(d1, -e);
+          e0 = __builtin_amdgcn_ldexp(e0, -e); e1 = __builtin_amdgcn_ldexp(e1, -e);
+        });
+        if (!(p1 != 0.0)) break;
+        const double G = d1 / p1, H = G * G - e1 / p1;
+        const double nn = static_cast<double>(m);
+        const double den = G + sqrt(fmax((nn - 1.0) * (nn * H - G * G), 0.0));
+        const double xn = x - nn / den;
+        if (!(xn < x) || !(xn >= llo)) break;
+        const bool fin = x - xn <= 4e-16 * fabs(x);
+        x = xn;
+        if (fin) break;
+      }
+      const double u = 64.0 * 2.2204460492503131e-16 * fabs(x);
+      if (x - u > lo && x + u < hi) {
+        lo = x - u;
+        hi = x + u;
+        laguerre = true;
+      }
+    }
+  }
+  stamp(0);
+  for (; !done && round < 48; ++round) {
+    const int kind = laguerre ? 3 : (hinted && hg < hi && round == 0 ? 1 : 0);
+    const bool was_l = laguerre;
+    done = mround(kind);
+    if (was_l) laguerre = false;
   }
   const double lm = 0.5 * (lo + hi);
+  stamp(1);
   // ---- the two eigenvector recurrences of (T - lm) f = 0 in the division-
   // free minor form (fast_check), forward from the top and backward from the
   // bottom, interleaved; rescaled by powers of two every four steps
@@ -191,47 +225,40 @@ __device__ __forceinline__ void wave_check(const double* T, int m, double theta_
     double* exb = ex + kExStride;
     double fg1 = 1.0, fg0 = 0.0, fq = 1.0, bg1 = 1.0, bg0 = 0.0, bq = 1.0, bbw = 0.0;
     int feg = 0, feq = 0, beg = 0, beq = 0;
-    double fgv[2] = {0.0, 0.0}, fqv[2] = {0.0, 0.0}, bgv[2] = {0.0, 0.0}, bqv[2] = {0.0, 0.0};
+    // chain values are wave-uniform: lane 0 stores each (g, Q) pair straight
+    // into the scratch (no per-lane select of the index's owner)
     if (lane == 0) {
-      fgv[0] = 1.0;
-      fqv[0] = 1.0;
       exf[0] = exf[1] = exb[0] = exb[1] = 0.0;
+      gq[0] = 1.0;
+      gq[MMAX] = 1.0;
+      hr[m - 1] = 1.0;
+      hr[MMAX + m - 1] = 1.0;
     }
-    if (((m - 1) & 63) == lane) {
-      if (m - 1 < 64) {
-        bgv[0] = 1.0;
-        bqv[0] = 1.0;
-      } else {
-        bgv[1] = 1.0;
-        bqv[1] = 1.0;
-      }
-    }
-    auto put = [&](double (&gv)[2], double (&qv)[2], int idx, double g, double q) __attribute__((always_inline)) {
-      const bool me = (idx & 63) == lane;
-      if (idx < 64) {
-        gv[0] = me ? g : gv[0];
-        qv[0] = me ? q : qv[0];
-      } else {
-        gv[1] = me ? g : gv[1];
-        qv[1] = me ? q : qv[1];
+    // chain values are wave-uniform: lane 0 stores them, a block of four steps
+    // at a time (one exec-mask region per block, so the steps' fp64 chains are
+    // scheduled without a branch between them)
+    auto put = [&](double* v, int idx, double g, double q) __attribute__((always_inline)) {
+      if (lane == 0) {
+        v[idx] = g;
+        v[MMAX + idx] = q;
       }
     };
-    // fwd row i = k: (alpha_k, behind beta^2_{k-1}), ahead beta^2_k; index k + 1
-    // bwd row i = m-1-k: alpha_i, ahead beta^2_{i-1} = T2[i].y, behind the
-    // previous pair's .y; index m - 2 - k
-    auto step = [&](int k) __attribute__((always_inline)) {
-      const double2 fc = T2[k], fn = T2[k + 1], bc = T2[m - 1 - k];
+    // forward step k: pair k (carried) and pair k + 1; backward step k: pair
+    // m - 1 - k; both streams read a block of four ahead (tstream)
+    double2 fc = T2[0];
+    auto step = [&](double2 fn, double2 bc) __attribute__((always_inline)) {
       const double fgn = fma(lm - fc.x, fg1, -(fc.y * fg0));
       fq *= fn.y;
       fg0 = fg1;
       fg1 = fgn;
+      fc = fn;
       const double bgn = fma(lm - bc.x, bg1, -(bbw * bg0));
       bq *= bc.y;
       bbw = bc.y;
       bg0 = bg1;
       bg1 = bgn;
     };
-    auto rescale = [&](int k) __attribute__((always_inline)) {
+    auto rescale_values = [&]() __attribute__((always_inline)) {
       int e = __builtin_amdgcn_frexp_exp(fg1);
       fg1 = __builtin_amdgcn_ldexp(fg1, -e);
       fg0 = __builtin_amdgcn_ldexp(fg0, -e);
@@ -246,46 +273,62 @@ __device__ __forceinline__ void wave_check(const double* T, int m, double theta_
       e = __builtin_amdgcn_frexp_exp(bq);
       bq = __builtin_amdgcn_ldexp(bq, -e);
       beq += e;
+    };
+    const int steps = m - 1;
+    // pair indices m-1-k for the backward stream are >= 0 for k < m; the reads
+    // past the chain's end (k >= steps) land on valid record slots and are unused
+    auto bidx = [&](int k) { return m - 1 - k < 0 ? 0 : m - 1 - k; };
+    double2 f0 = T2[1], f1 = T2[2], f2 = T2[3], f3 = T2[4];
+    double2 b0 = T2[bidx(0)], b1 = T2[bidx(1)], b2 = T2[bidx(2)], b3 = T2[bidx(3)];
+    int k = 0;
+    for (; k + 4 <= steps; k += 4) {
+      const double2 nf0 = T2[k + 5], nf1 = T2[k + 6], nf2 = T2[k + 7], nf3 = T2[k + 8];
+      const double2 nb0 = T2[bidx(k + 4)], nb1 = T2[bidx(k + 5)], nb2 = T2[bidx(k + 6)], nb3 = T2[bidx(k + 7)];
+      double sg[4], sq[4], sh[4], sr[4];
+      step(f0, b0);
+      sg[0] = fg1; sq[0] = fq; sh[0] = bg1; sr[0] = bq;
+      step(f1, b1);
+      sg[1] = fg1; sq[1] = fq; sh[1] = bg1; sr[1] = bq;
+      step(f2, b2);
+      sg[2] = fg1; sq[2] = fq; sh[2] = bg1; sr[2] = bq;
+      step(f3, b3);
+      rescale_values();
+      sg[3] = fg1; sq[3] = fq; sh[3] = bg1; sr[3] = bq;
       if (lane == 0) {
-        const int b = 2 * ((k + 1) >> 2);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          gq[k + 1 + u] = sg[u];
+          gq[MMAX + k + 1 + u] = sq[u];
+          hr[m - 2 - k - u] = sh[u];
+          hr[MMAX + m - 2 - k - u] = sr[u];
+        }
+        const int b = 2 * ((k + 4) >> 2);
         exf[b] = static_cast<double>(feg);
         exf[b + 1] = static_cast<double>(feq);
         exb[b] = static_cast<double>(beg);
         exb[b + 1] = static_cast<double>(beq);
       }
-    };
-    const int steps = m - 1;
-    int k = 0;
-    for (; k + 4 <= steps; k += 4) {
-      step(k);
-      put(fgv, fqv, k + 1, fg1, fq);
-      put(bgv, bqv, m - 2 - k, bg1, bq);
-      step(k + 1);
-      put(fgv, fqv, k + 2, fg1, fq);
-      put(bgv, bqv, m - 3 - k, bg1, bq);
-      step(k + 2);
-      put(fgv, fqv, k + 3, fg1, fq);
-      put(bgv, bqv, m - 4 - k, bg1, bq);
-      step(k + 3);
-      rescale(k + 3);
-      put(fgv, fqv, k + 4, fg1, fq);
-      put(bgv, bqv, m - 5 - k, bg1, bq);
+      f0 = nf0; f1 = nf1; f2 = nf2; f3 = nf3;
+      b0 = nb0; b1 = nb1; b2 = nb2; b3 = nb3;
     }
-    for (; k < steps; ++k) {
-      step(k);
-      put(fgv, fqv, k + 1, fg1, fq);
-      put(bgv, bqv, m - 2 - k, bg1, bq);
+    if (k < steps) {
+      step(f0, b0);
+      put(gq, k + 1, fg1, fq);
+      put(hr, m - 2 - k, bg1, bq);
     }
-    gq[lane] = fgv[0];
-    gq[64 + lane] = fgv[1];
-    gq[MMAX + lane] = fqv[0];
-    gq[MMAX + 64 + lane] = fqv[1];
-    hr[lane] = bgv[0];
-    hr[64 + lane] = bgv[1];
-    hr[MMAX + lane] = bqv[0];
-    hr[MMAX + 64 + lane] = bqv[1];
+    if (k + 1 < steps) {
+      step(f1, b1);
+      put(gq, k + 2, fg1, fq);
+      put(hr, m - 3 - k, bg1, bq);
+    }
+    if (k + 2 < steps) {
+      step(f2, b2);
+      put(gq, k + 3, fg1, fq);
+      put(hr, m - 4 - k, bg1, bq);
+    }
   }
   wsym::lds_order();   // every lane reads its neighbours' chain values
+  stamp(2);
   auto pexp = [&](const double* exb, int p, int which) -> int { return static_cast<int>(exb[2 * (p >> 2) + which]); };
   const double* exf = ex;
   const double* exb = ex + kExStride;
@@ -345,6 +388,7 @@ __device__ __forceinline__ void wave_check(const double* T, int m, double theta_
   if (lane < m) z[lane] = zv[0] * inv;
   if (lane + 64 < m) z[lane + 64] = zv[1] * inv;
   wsym::lds_order();
+  stamp(3);
   *zlast_out = rl_any(zv, m - 1) * inv;
   *theta_out = lm;
   *rounds_out = round + 1;
@@ -465,7 +509,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
       bool converged = false;
       double tscale = 0.0;
-      long long tcheck = 0, tmv = 0, tstep = 0;
+      long long tcheck = 0, tmv = 0, tstep = 0, tph[4] = {0, 0, 0, 0};
       int trounds = 0;
       // attempt 0: plain Lanczos; 1: after a ghost, again with dense checks;
       // 2: with full re-orthogonalisation against the stored basis
@@ -490,15 +534,22 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         // that accepts has spent one step for nothing.
         for (int j = 0;; ++j) {
           const long long ts0 = dbg ? clock64() : 0;
-          double y0, y1;
-          {
-            const double z0 = sw0 * rt0, z1 = sw1 * rt1;
-            wsym::put_operand(zd, z0, z1);
-            wsym::matvec<WKV>(P, cl, zd, tb, z0, z1, y0, y1);
-          }
+          // beta_j first in program order: its reduction, root and reciprocal
+          // depend only on r~_j, so they fill the matvec's latency gaps
           const double nrm2 = wave_sum(rt0 * rt0 + rt1 * rt1);
           const double bet = sqrt(nrm2);
           const double ib = 1.0 / bet;
+          double my0, my1;   // (M r~_j) = W^1/2 C W^1/2 r~_j
+          {
+            const double z0 = sw0 * rt0, z1 = sw1 * rt1;
+            double y0, y1;
+            wsym::put_operand(zd, z0, z1);
+            wsym::matvec<WKV>(P, cl, zd, tb, z0, z1, y0, y1);
+            my0 = sw0 * y0;
+            my1 = sw1 * y1;
+          }
+          // alpha_j beta_j^2 = r~_j . M r~_j: reduced without waiting for 1/beta_j
+          const double pa = wave_sum(rt0 * my0 + rt1 * my1);
           const long long ts1 = dbg ? clock64() : 0;
           if (dbg) tmv += ts1 - ts0;
           trw[2 * j + 1] = nrm2;   // every lane stores the same value (no exec-mask branch); T[1] is never used
@@ -514,8 +565,8 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
           // step whose check ends the attempt is stored and never read)
           const double q0 = rt0 * ib, q1 = rt1 * ib;
           reinterpret_cast<double2*>(Vb + j * FNP)[lane] = double2{q0, q1};
-          const double mq0 = sw0 * y0 * ib, mq1 = sw1 * y1 * ib;
-          double aj = wave_sum(q0 * mq0 + q1 * mq1);
+          const double mq0 = my0 * ib, mq1 = my1 * ib;
+          double aj = pa * ib * ib;
           double n0 = mq0 - aj * q0 - (j > 0 ? bet * qp0 : 0.0);
           double n1 = mq1 - aj * q1 - (j > 0 ? bet * qp1 : 0.0);
           if (reorth) {
@@ -564,7 +615,8 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
             const long long tc0 = dbg ? clock64() : 0;
             double lm, zl;
             int rounds = 0;
-            wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, scr, &lm, &zl, &rounds);
+            wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, scr, &lm, &zl, &rounds,
+                       dbg ? tph : nullptr);
             if (dbg) {
               tcheck += clock64() - tc0;
               trounds += rounds;
@@ -628,8 +680,22 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       {
         const double* zb = zbuf + zbest * MMAX;
         const double2* V2 = reinterpret_cast<const double2*>(Vb);
+        // eight basis rows in flight per batch (the scratch is in L2 / the
+        // Infinity Cache: one load latency per batch, not per row)
         double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
         int qq = 0;
+        for (; qq + 8 <= m_conv; qq += 8) {
+          double2 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = V2[(qq + u) * 64 + lane];
+#pragma unroll
+          for (int u = 0; u < 8; u += 2) {
+            a0 = fma(zb[qq + u], v[u].x, a0);
+            a1 = fma(zb[qq + u], v[u].y, a1);
+            b0 = fma(zb[qq + u + 1], v[u + 1].x, b0);
+            b1 = fma(zb[qq + u + 1], v[u + 1].y, b1);
+          }
+        }
         for (; qq + 1 < m_conv; qq += 2) {
           const double za = zb[qq], zb1 = zb[qq + 1];
           const double2 va = V2[qq * 64 + lane], vb = V2[(qq + 1) * 64 + lane];
@@ -658,8 +724,10 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
           rec[FNP + 3] = nchecks;
           rec[FNP + 4] = nact;
           rec[FNP + 5] = sgw;
-          rec[FNP + 6] = 0;
-          rec[FNP + 7] = 0;
+          rec[FNP + 6] = static_cast<double>(tph[0]);   // check phases: Laguerre, multisection,
+          rec[FNP + 7] = static_cast<double>(tph[1]);   // eigenvector chains, twist + z
+          rec[FNP + 13] = static_cast<double>(tph[2]);
+          rec[FNP + 14] = static_cast<double>(tph[3]);
           rec[FNP + 8] = static_cast<double>(clock64() - t_it);
           rec[FNP + 9] = static_cast<double>(tcheck);
           rec[FNP + 10] = static_cast<double>(tmv);

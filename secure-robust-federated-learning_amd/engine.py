@@ -317,6 +317,11 @@ def _filter(X, mode, eps, sigma, expansion, itv, check, out=None, info=None):
     ws = _workspace(nb, X.device)
     _lib.call("sra_filter_f32", X.data_ptr(), n, d, ldx, int(mode), w, float(eps), float(sigma),
               float(expansion), out.data_ptr(), status.data_ptr(), ws.data_ptr(), nb, _stream_ptr(X.device))
+    _filter_status(status, mode, check, info, d, w)
+    return out
+
+
+def _filter_status(status, mode, check, info, d, w):
     if check or info is not None:
         st = status.cpu().tolist()
         if check and st[0] == 2:
@@ -326,7 +331,6 @@ def _filter(X, mode, eps, sigma, expansion, itv, check, out=None, info=None):
         if info is not None:
             info["unweighted_chunks"] = int(st[1])
             info["chunks"] = -(-d // w)
-    return out
 
 
 FILTER_TRACE_STRIDE = 1 + 2 * 128
@@ -397,18 +401,39 @@ def mom_bucket_count(n, eps, delta):
     return num, size
 
 
-def mom_filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True,
-                  out=None):
+def _mom_filter(X, mode, eps, sigma, expansion, itv, delta, check, out, info=None):
+    """The MoM forms (robust_estimator.py:135-142, 210-218): up to 128 buckets
+    in one call whose chunk-Gram loads form the bucket means (sra_mom_filter_f32,
+    the bucket matrix never written whole); more buckets through the bucket
+    kernel and the N > 128 filter."""
     n = int(X.shape[0])
     num, size = mom_bucket_count(n, eps, delta)
-    return filter_l2(bucket_means(X, size, num), eps, sigma, expansion, itv, check, out)
+    if num > 128:
+        return _filter(bucket_means(X, size, num), mode, eps, sigma, expansion, itv, check, out, info)
+    X, n, d, ldx = as_matrix(X)
+    if out is None:
+        out = torch.empty(d, dtype=torch.float64, device=X.device)
+    elif out.dtype != torch.float64 or out.numel() != d or not out.is_contiguous() or out.device != X.device:
+        raise ValueError("out must be a contiguous float64 (d,) tensor on X's device")
+    status = torch.zeros(2, dtype=torch.int32, device=X.device)
+    w = chunk_width(d, itv)
+    nb = _lib.query_bytes("sra_mom_filter_workspace_bytes", num, d, w)
+    ws = _workspace(nb, X.device)
+    _lib.call("sra_mom_filter_f32", X.data_ptr(), n, d, ldx, int(mode), w, int(size), int(num), float(eps),
+              float(sigma), float(expansion), out.data_ptr(), status.data_ptr(), ws.data_ptr(), nb,
+              _stream_ptr(X.device))
+    _filter_status(status, mode, check, info, d, w)
+    return out
+
+
+def mom_filter_l2(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True,
+                  out=None):
+    return _mom_filter(X, 0, eps, sigma, expansion, itv, delta, check, out)
 
 
 def mom_ex_noregret(X, eps=0.2, sigma=1, expansion=20, itv=ITV, delta=2.718281828459045 ** -30, check=True,
                     out=None, info=None):
-    n = int(X.shape[0])
-    num, size = mom_bucket_count(n, eps, delta)
-    return ex_noregret(bucket_means(X, size, num), eps, sigma, expansion, itv, check, out, info)
+    return _mom_filter(X, 1, eps, sigma, expansion, itv, delta, check, out, info)
 
 
 # ---------------------------------------------------------------------------

@@ -52,6 +52,50 @@ def _world(group):
     return dist.get_world_size(group), dist.get_rank(group)
 
 
+# Collectives.  A gloo group over GPU ranks (several ranks sharing one GPU, as
+# the two-rank execution test of tests/test_gpu_shard2.py runs them; RCCL
+# refuses two ranks on one device) stages device tensors through host memory;
+# an RCCL group takes the device tensors directly.
+def _staged(t, group):
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _all_gather_into(out, inp, group=None):
+    if _staged(inp, group):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def _all_reduce(t, group=None):
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+
+
+def _reduce(t, dst, group=None):
+    if _staged(t, group):
+        h = t.cpu()
+        dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def _broadcast(t, src, group=None):
+    if _staged(t, group):
+        h = t.cpu()
+        dist.broadcast(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src, group=group)
+
+
 def gather_columns(local, d, align=1, group=None):
     """All-gather per-rank column blocks (1-D ``local`` of length hi-lo, or
     2-D with columns last) into the full d-vector on every rank."""
@@ -67,7 +111,7 @@ def gather_columns(local, d, align=1, group=None):
     if not dist.is_initialized():
         return padded[..., :d].clone()
     gathered = torch.empty((world,) + lead + (width,), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(gathered, padded.unsqueeze(0).contiguous(), group=group)
+    _all_gather_into(gathered, padded.unsqueeze(0).contiguous(), group)
     parts = [gathered[r][..., :bh - bl] for r, (bl, bh) in enumerate(bounds)]
     return torch.cat(parts, dim=-1)
 
@@ -86,11 +130,11 @@ def _gram_pick(G, pick, count, group=None):
         return pick(G)
     _, rank = _world(group)
     root = dist.get_global_rank(group, 0) if group is not None else 0
-    dist.reduce(G, dst=root, op=dist.ReduceOp.SUM, group=group)
+    _reduce(G, root, group)
     idx = torch.zeros(count, dtype=torch.int64, device=G.device)
     if rank == 0:
         idx.copy_(torch.as_tensor(pick(G), device=G.device).reshape(count).to(torch.int64))
-    dist.broadcast(idx, src=root, group=group)
+    _broadcast(idx, root, group)
     return idx
 
 
@@ -167,7 +211,7 @@ def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
             nr = n - t
             dvec = ops["bulyan_round"](X_shard, rows, nr, aggsubfunc, S[t])
             if on:
-                dist.all_reduce(dvec, op=dist.ReduceOp.SUM, group=group)
+                _all_reduce(dvec, group)
             ops["bulyan_pick"](dvec, rows, nr, nxt, status)
             rows, nxt = nxt, rows
         if int(status.item()) != 0:
@@ -236,9 +280,9 @@ def pipelined_coordinatewise(local_fn, X_local, d, block, group=None, out=None, 
             ev.record(compute)
             with torch.cuda.stream(comm_stream):
                 comm_stream.wait_event(ev)
-                dist.all_gather_into_tensor(full[k * span:(k + 1) * span], seg, group=group)
+                _all_gather_into(full[k * span:(k + 1) * span], seg, group)
         else:
-            dist.all_gather_into_tensor(full[k * span:(k + 1) * span], seg, group=group)
+            _all_gather_into(full[k * span:(k + 1) * span], seg, group)
     if cuda:
         compute.wait_stream(comm_stream)
         full.record_stream(comm_stream)

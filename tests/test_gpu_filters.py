@@ -50,14 +50,17 @@ def test_golden_filters(rec):
             call(xs, rec["params"])
         return
     if rec["name"] == "ex_noregret_none_exit":
-        # projected_c = None at iteration 0; the reference's next iteration
-        # (weights=None) evaluates the same covariance in fp32 and, with sigma
-        # tuned into the 1e-7 rounding gap between that fp32 eigenvalue and
-        # iteration 0's fp64 one, exits with the fp32 mean.  The engine carries
-        # the None state into a uniform-weight iteration too, but its fp64
-        # eigenvalue sits on iteration 0's side of that gap: either outcome of
-        # the reference's own rounding is accepted, and a returned value must
-        # be the unweighted mean.
+        # projected_c = None at iteration 0 (robust_estimator.py:99); the
+        # reference's next iteration (weights=None) runs in fp32 (fp32 mean,
+        # covariance and eigh) and this sigma sits inside the ~1e-7-wide window
+        # between that fp32 eigenvalue and iteration 0's fp64 one, so the
+        # reference exits with the fp32 mean.  Which side of the window an
+        # evaluation lands on is LAPACK's fp32 rounding: no fp64 solver can
+        # reproduce it.  Both sides of the window ARE
+        # pinned exactly by ex_noregret_none_below (TypeError) and
+        # ex_noregret_exit_above (the fp64 exit at iteration 0),
+        # tests/golden/gen_none_sides.py; here a returned value must be the
+        # unweighted fp32 mean and anything else must be the TypeError.
         try:
             got = call(xs, rec["params"])
         except TypeError:

@@ -55,6 +55,8 @@ if len(sys.argv) > 2 and sys.argv[2] == "synthetic":
         print("   checks", sum(ck), "second GS passes", sum(p2), "restarts", int(recs[:len(ms), 134].sum()))
         print("   resid", [float("%.1e" % recs[i, 130]) for i in range(len(ms))][:10])
         print("   Mcycles/iteration %.3f, cycles per Lanczos step %.0f" % (np.mean(cyc) / 1e6, sum(cyc) / max(1, sum(ms))))
+        cp = recs[:len(ms), [134, 135, 141, 142]].numpy().sum(0)
+        print("   per check: Laguerre %.0f  multisection %.0f  chains %.0f  twist+z %.0f cycles" % tuple(cp / max(1, sum(ck))))
         ph = recs[:len(ms), 137:141].numpy().sum(0)
         print("   per step: check %.0f  matvec+alpha %.0f  dots %.0f  update+reduce %.0f cycles" % tuple(ph / max(1, sum(ms))))
         for d in (1000, 10_000_000):
