@@ -2765,10 +2765,6 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
   const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
                            : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
   SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLdsTotal)));
-  // ex_noregret stays on the re-orthogonalising kernel: on the plain solver
-  // (217 vs 327 ms at C4) every traced decision agreed, but the C4 fixture
-  // chunk 1 landed 2.9e-3 of max from the reference (bound 2e-5) and two DBA
-  // fixtures missed rtol 1e-5 (DESIGN k6)
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
     GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws, bs, nsrc, Bws, ldb};
@@ -2793,18 +2789,10 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
                  kMaxAdvance, 0};
     SRA_HIP(hipMemsetAsync(fbc, 0, 8 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
-    if (mode == 1) {
-      // round 2: ex_noregret's top two eigenvalues close in (gaps ~1e-3 after a
-      // few iterations) and plain Lanczos without the re-orthogonalising
-      // attempt stalled above the accuracy floor in a third of the chunks:
-      // every chunk on the re-orthogonalising solver
-      hipLaunchKernelGGL(list_all_kernel, dim3(cdiv(nb, 256)), dim3(256), 0, s, fbl, fbc, nb);
-      rc = launch_status("list_all_kernel");
-      if (rc) return rc;
-    } else {
-      rc = launch_wave_solve(dbg != nullptr, sa, lgrid, s);
-      if (rc) return rc;
-    }
+    // both filters on the one-wave solver (ex_noregret re-orthogonalising
+    // from the first step, wave_solve_kernel<1>)
+    rc = launch_wave_solve(mode, dbg != nullptr, sa, lgrid, s);
+    if (rc) return rc;
     // the listed chunks (not converged / ghost) on the re-orthogonalising solver
     const int grid = nb < 512 ? nb : 512;
     if (mode == 0 && dbg) hipLaunchKernelGGL((filter_solve_kernel<0, true>), dim3(grid), dim3(256), kSolveLds, s, sa);

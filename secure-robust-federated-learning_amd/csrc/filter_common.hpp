@@ -143,6 +143,6 @@ __device__ __forceinline__ double rcp_nr(double b) {   // 1/b within ~1 ulp
 // filter_wave.hip: the one-wave filterL2 solver (round 5)
 size_t wave_solve_lds();
 int wave_solve_grid();
-int launch_wave_solve(bool dbg, const SolveArgs& sa, int grid, hipStream_t s);
+int launch_wave_solve(int mode, bool dbg, const SolveArgs& sa, int grid, hipStream_t s);
 
 }  // namespace sra

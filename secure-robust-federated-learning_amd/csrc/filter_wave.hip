@@ -55,6 +55,8 @@ constexpr int kWTrw = 2 * MMAX + 32;          // T record: (alpha_q, beta^2_{q-1
 constexpr size_t kWaveLds = sizeof(double) * (static_cast<size_t>(WKL) * FNP + kWScr + kWTrw + 2 * MMAX);
 static_assert(4 * kWaveLds <= 163840, "four one-wave solvers must fit one CU's LDS");
 constexpr int kWaveGrid = 1024;               // 4 waves per CU x 256 CUs; each owns a basis slot
+constexpr double kEps = 1.1102230246251565e-16;       // unit roundoff
+constexpr double kSqrtEps = 1.0536712127723509e-08;   // sqrt(kEps): the semi-orthogonality bound
 
 // The pairs T2[q] = (alpha_q, beta^2 of (q-1, q)) for q = 1 .. m-1 into f, g()
 // after every fourth: the next block's four LDS reads are issued before the
@@ -438,9 +440,144 @@ __device__ __forceinline__ int wave_argmax_first(double v, int i, double* vbest)
   return __builtin_amdgcn_readfirstlane(i);
 }
 
+// ---- eight wave sums at once ------------------------------------------------
+// h[i] = sum over the wave of p[i], wave-uniform.  A reduce-scatter halves the
+// values per lane at every level -- v_permlane32_swap (lane ^ 32), then
+// v_permlane16_swap (rows 0/2 vs 1/3), then DPP row_ror:8 (lane ^ 8) -- so
+// the last three levels are one value's DPP sum over eight lanes, and value
+// i ends in lanes 8i .. 8i + 7 (13 cross-lane moves and adds per value pair
+// instead of wave_sum's 8 DPP moves + 8 readlanes per value).
+__device__ __forceinline__ void swap_rows(double& a, double& b, bool wide) {
+  const unsigned long long ua = __builtin_bit_cast(unsigned long long, a), ub = __builtin_bit_cast(unsigned long long, b);
+  const unsigned al = static_cast<unsigned>(ua), ah = static_cast<unsigned>(ua >> 32);
+  const unsigned bl = static_cast<unsigned>(ub), bh = static_cast<unsigned>(ub >> 32);
+  unsigned nal, nah, nbl, nbh;
+  if (wide) {   // lanes 32-63 of a <-> lanes 0-31 of b
+    const auto lo = __builtin_amdgcn_permlane32_swap(al, bl, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(ah, bh, false, false);
+    nal = lo[0]; nbl = lo[1]; nah = hi[0]; nbh = hi[1];
+  } else {      // odd rows of a <-> even rows of b
+    const auto lo = __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+    nal = lo[0]; nbl = lo[1]; nah = hi[0]; nbh = hi[1];
+  }
+  a = __builtin_bit_cast(double, (static_cast<unsigned long long>(nah) << 32) | nal);
+  b = __builtin_bit_cast(double, (static_cast<unsigned long long>(nbh) << 32) | nbl);
+}
+
+__device__ __forceinline__ void wave_sum8(const double (&p)[8], double (&h)[8]) {
+  const int lane = threadIdx.x & 63;
+  double q[4], r[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {   // lanes < 32: value i, lanes >= 32: value i + 4
+    double a = p[i], b = p[i + 4];
+    swap_rows(a, b, true);
+    q[i] = a + b;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {   // even rows: q[i]'s value, odd rows: q[i + 2]'s
+    double a = q[i], b = q[i + 2];
+    swap_rows(a, b, false);
+    r[i] = a + b;
+  }
+  // lanes 0-7 of a row keep r[0], lanes 8-15 keep r[1]; each takes the other
+  // half's copy of the value it keeps
+  const bool upper = (lane & 8) != 0;
+  const double keep = upper ? r[1] : r[0], send = upper ? r[0] : r[1];
+  double v = keep + dpp_f64<0x128>(send);   // row_ror:8
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = readlane_f64(v, 8 * i);
+}
+
+// ---- ex_noregret's KL projection, one wave (kl_project_t in filter.hip) ---
+// {c : sum c = 1, c <= cap} over the nk kept clients (robust_estimator.py:
+// 74-99): candidate i caps the i + 1 largest weights and rescales the rest;
+// the feasible candidate with the smallest KL wins (first on ties), the
+// reference's loop stops at the first infeasible clip.  Lane l: rows 2l,
+// 2l + 1 and the compact entries / candidates l, l + 64.  scr: 512 doubles.
+// Returns false when no candidate is feasible (projected_c = None, :99).
+__device__ bool wave_kl_project(double& c0, double& c1, bool ai0, bool ai1, int nk, double cap, double* scr,
+                                int* capped) {
+  const int lane = threadIdx.x & 63;
+  double* cc = scr;                                      // [FNP] compact weights
+  double* sv = scr + FNP;                                // [FNP] weights in descending order
+  double* hl = scr + 2 * FNP;                            // [FNP] sv log(sv / cap)
+  int* irank = reinterpret_cast<int*>(scr + 3 * FNP);    // [FNP] descending rank of a compact entry
+  const unsigned long long m0 = __builtin_amdgcn_ballot_w64(ai0), m1 = __builtin_amdgcn_ballot_w64(ai1);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const int pos0 = __builtin_popcountll(m0 & below) + __builtin_popcountll(m1 & below);
+  const int pos1 = pos0 + (ai0 ? 1 : 0);
+  wsym::lds_order();
+  if (ai0) cc[pos0] = c0;
+  if (ai1) cc[pos1] = c1;
+  wsym::lds_order();
+  // descending rank; ties: later compact index first (flip of a stable ascending argsort)
+  const int t0 = lane, t1 = lane + 64;
+  const double v0 = t0 < nk ? cc[t0] : 0.0, v1 = t1 < nk ? cc[t1] : 0.0;
+  int rk0 = 0, rk1 = 0;
+  for (int q = 0; q < nk; ++q) {
+    const double cq = cc[q];
+    rk0 += (cq > v0 || (cq == v0 && q > t0)) ? 1 : 0;
+    rk1 += (cq > v1 || (cq == v1 && q > t1)) ? 1 : 0;
+  }
+  if (t0 < nk) {
+    irank[t0] = rk0;
+    sv[rk0] = v0;
+    hl[rk0] = v0 * log(v0 / cap);
+  }
+  if (t1 < nk) {
+    irank[t1] = rk1;
+    sv[rk1] = v1;
+    hl[rk1] = v1 * log(v1 / cap);
+  }
+  wsym::lds_order();
+  double negkl[2] = {-__builtin_inf(), -__builtin_inf()}, scale[2] = {0.0, 0.0};
+  int stop = 1 << 30;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int i = lane + 64 * s;
+    if (i < nk) {
+      const double clip = 1.0 - np_pw64(0, i + 1, [&](int) { return cap; });
+      if (clip <= 0.0) {
+        stop = stop < i ? stop : i;
+      } else if (i + 1 < nk) {
+        const double norm = np_pw64(i + 1, nk - i - 1, [&](int q) { return sv[q]; });
+        scale[s] = clip / norm;
+        if (!(sv[i + 1] * scale[s] > cap)) {
+          double head = 0.0;
+          for (int q = 0; q <= i; ++q) head += hl[q];
+          negkl[s] = -(head - norm * log(scale[s]));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int o2 = __shfl_xor(stop, off);
+    stop = o2 < stop ? o2 : stop;
+  }
+  stop = __builtin_amdgcn_readfirstlane(stop);
+  if (lane >= stop) negkl[0] = -__builtin_inf();
+  if (lane + 64 >= stop) negkl[1] = -__builtin_inf();
+  const bool take1 = negkl[1] > negkl[0];   // ties: the lower candidate index
+  double best;
+  const int bi = wave_argmax_first(take1 ? negkl[1] : negkl[0], take1 ? lane + 64 : lane, &best);
+  const bool ok = best > -__builtin_inf();
+  *capped = ok ? bi + 1 : 0;
+  if (ok) {
+    const double sb = readlane_f64(bi < 64 ? scale[0] : scale[1], bi & 63);
+    if (ai0) c0 = irank[pos0] <= bi ? cap : cc[pos0] * sb;
+    if (ai1) c1 = irank[pos1] <= bi ? cap : cc[pos1] * sb;
+  }
+  wsym::lds_order();   // the scratch is the next check's
+  return ok;
+}
+
 template <int MODE, bool DBG>
 __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
-  static_assert(MODE == 0, "ex_noregret stays on filter_solve_kernel");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* cl = reinterpret_cast<double*>(smem);   // [WKL][FNP] C's LDS diagonals
   double* scr = cl + WKL * FNP;                   // [kWScr] operand + group shifts | check scratch
@@ -476,9 +613,24 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       });
     }
     bool ai0 = r0 < n, ai1 = r1 < n;
+    if constexpr (MODE == 1) {   // the kept set of the pre-filter (noregret_pre_kernel)
+      const int2 a2 = reinterpret_cast<const int2*>(A.act + static_cast<size_t>(ch) * FNP)[lane];
+      ai0 = ai0 && a2.x != 0;
+      ai1 = ai1 && a2.y != 0;
+    }
     double ci0 = ai0 ? 1.0 : 0.0, ci1 = ai1 ? 1.0 : 0.0;
-    const int iters = 2 * static_cast<int>(A.eps * n);
-    int m_hint = 24;
+    const int fdrop = static_cast<int>(ceil(A.eps * n));
+    const int n_keep = MODE == 1 ? n - (fdrop < n ? fdrop : n) : n;
+    const double step = MODE == 1 ? A.misc[static_cast<size_t>(ch) * kMisc + 1] : 0.0;
+    const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n) : static_cast<int>(2 * A.eps * n_keep);
+    // ex_noregret: projected_c = None (no feasible candidate, :99): the next
+    // iteration runs with weights=None (the plain mean and covariance,
+    // :65-67) and either exits with that mean (:71-72) or fails at
+    // c * (1 - step * tau) (:75, TypeError); at the last iteration the final
+    // np.average(weights=None) returns it (:101)
+    bool none = false, unweighted = false, have_u = false;
+    double u0 = 0.0, u1 = 0.0;   // the last Ritz vector (rows 2 lane, 2 lane + 1)
+    int m_hint = MODE == 1 ? 12 : 24;
     double rate_hint = 0.0;
     bool fallback = false;
     int done = 0;
@@ -488,6 +640,10 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
 
     for (int it = 0; it < iters; ++it) {
       const long long t_it = dbg ? clock64() : 0;
+      if (MODE == 1 && none) {
+        ci0 = ai0 ? 1.0 : 0.0;
+        ci1 = ai1 ? 1.0 : 0.0;
+      }
       // ---- weights, and C recentred at the weighted mean
       const double csum = wave_sum((ai0 ? ci0 : 0.0) + (ai1 ? ci1 : 0.0));
       const int nact = static_cast<int>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(ai0)) +
@@ -505,7 +661,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       }
 
       // ---- top eigenpair of M = W^1/2 C W^1/2 by plain Lanczos
-      double lam = 0.0, resid = 0.0, u0 = 0.0, u1 = 0.0;
+      double lam = 0.0, resid = 0.0;
       int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
       bool converged = false;
       double tscale = 0.0;
@@ -513,19 +669,98 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       int trounds = 0;
       // attempt 0: plain Lanczos; 1: after a ghost, again with dense checks;
       // 2: with full re-orthogonalisation against the stored basis
+      // ex_noregret (MODE 1) re-orthogonalises from the start: its weights
+      // integrate every iteration's eigenvector and its top two eigenvalues
+      // close in (gaps ~1e-3 after a few iterations), where plain Lanczos
+      // stalled above the accuracy floor
+      // block Gram-Schmidt of r~ = (n0, n1) against q_0 .. q_j, eight vectors
+      // per block (one wave_sum8 for their coefficients, then their update, so
+      // a block is read once per pass); q_j from registers, the others read
+      // back from the scratch (a lane reads only the entries it stored:
+      // program order suffices).  A second pass when |r|^2 drops below half
+      // (DGKS: |r - V h|^2 = |r|^2 - |h|^2); alpha takes the q_j coefficients.
+      int ngs = 0;   // debug records: full Gram-Schmidt calls
+      auto gs = [&](int j, double q0, double q1, double& n0, double& n1, double& aj) {
+        if (DBG) ++ngs;
+        const double2* V2 = reinterpret_cast<const double2*>(Vb);
+        for (int pass = 0; pass < 2; ++pass) {
+          const double nb2 = wave_sum(n0 * n0 + n1 * n1);
+          double hn2 = 0.0;
+          for (int qb = 0; qb <= j; qb += 8) {
+            double2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int q = qb + u;
+              const double2 b = V2[(q < j ? q : 0) * 64 + lane];
+              v[u] = q < j ? b : (q == j ? double2{q0, q1} : double2{0.0, 0.0});
+            }
+            double p[8], h[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = fma(v[u].x, n0, v[u].y * n1);
+            wave_sum8(p, h);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              n0 = fma(-h[u], v[u].x, n0);
+              n1 = fma(-h[u], v[u].y, n1);
+              hn2 = fma(h[u], h[u], hn2);
+              aj += qb + u == j ? h[u] : 0.0;
+            }
+          }
+          if (!(pass == 0 && nb2 - hn2 < kDgks * nb2)) break;
+        }
+      };
       for (int attempt = 0; attempt < 3 && !converged; ++attempt) {
-        const bool reorth = attempt == 2;
-        double rt0 = sw0 > 0.0 ? sw0 * hh0 : 0.0, rt1 = sw1 > 0.0 ? sw1 * hh1 : 0.0;
+        const bool full = attempt == 2;            // full re-orthogonalisation every step
+        const bool pro = MODE == 1 && !full;       // partial (omega recurrence)
+        const bool reorth = full || pro;
+        const double acc = MODE == 1 ? kResTol : kAccept;
+        // ex_noregret damps the top direction gently: the previous Ritz vector
+        // (perturbed) is a near-eigenvector of the next M
+        const bool warm = MODE == 1 && have_u && attempt == 0;
+        double rt0 = sw0 > 0.0 ? (warm ? u0 + 1e-3 * sw0 * hh0 : sw0 * hh0) : 0.0;
+        double rt1 = sw1 > 0.0 ? (warm ? u1 + 1e-3 * sw1 * hh1 : sw1 * hh1) : 0.0;
         double qp0 = 0.0, qp1 = 0.0, theta_lb = -1e300, hint = -1.0;
         double res_best = 1e300, lam_best = 0.0;
         tscale = 0.0;
         double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
         const int adv_max = attempt == 1 ? 1 : A.max_adv;
-        const int first = m_hint + A.first_off > 4 ? m_hint + A.first_off : 4;
+        const int off = MODE == 1 ? -1 : A.first_off;
+        const int first = m_hint + off > 4 ? m_hint + off : 4;
         int next_check = attempt == 1 ? (m_retry > 4 ? m_retry : 4) : first;
         int m_a = -1, m_last = 4, m_pre = 4;
         double res_a = 0.0;
         bool ghost = false;
+        // PRO state: |r~_j|^2 (computed at the end of step j - 1), and per lane
+        // k = lane, lane + 64: omega_{j,k}, omega_{j-1,k}, alpha_k, beta_k, beta_{k+1}
+        double nrm_c = pro ? wave_sum(rt0 * rt0 + rt1 * rt1) : 0.0;
+        double oc[2] = {lane == 0 ? 1.0 : 0.0, 0.0}, op[2] = {0.0, 0.0};
+        double al[2] = {0.0, 0.0}, be[2] = {0.0, 0.0}, be1[2] = {0.0, 0.0};
+        bool force = false;
+        // omega_{j+1,k} = (beta_{k+1} omega_{j,k+1} + (alpha_k - alpha_j) omega_{j,k}
+        //   + beta_k omega_{j,k-1} - beta_j omega_{j-1,k}) / beta_{j+1}, grown by
+        // eps (beta_{k+1} + beta_{j+1}) / beta_{j+1}; omega_{j+1,j} = eps sqrt(n) |T| /
+        // beta_{j+1}.  Returns max_k<=j |omega_{j+1,k}| and shifts the rows.
+        auto omega_step = [&](int j, double aj, double bj, double bn, double tn) -> double {
+          const int up = (lane + 1) & 63, dn = (lane + 63) & 63;
+          const double u0 = __shfl(oc[0], up), u1 = __shfl(oc[1], up);
+          const double d0 = __shfl(oc[0], dn), d1 = __shfl(oc[1], dn);
+          const double kp[2] = {lane < 63 ? u0 : u1, lane < 63 ? u1 : 0.0};
+          const double km[2] = {lane > 0 ? d0 : 0.0, lane > 0 ? d1 : d0};
+          const double ibn = 1.0 / bn;
+          const double psi = kEps * sqrt(static_cast<double>(nact)) * tn * ibn;
+          double mx = 0.0;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int k = lane + 64 * s2;
+            double w = (be1[s2] * kp[s2] + (al[s2] - aj) * oc[s2] + be[s2] * km[s2] - bj * op[s2]) * ibn;
+            w += copysign(kEps * (be1[s2] + bn) * ibn, w);
+            w = k < j ? w : (k == j ? psi : (k == j + 1 ? 1.0 : 0.0));
+            mx = k <= j ? fmax(mx, fabs(w)) : mx;
+            op[s2] = oc[s2];
+            oc[s2] = w;
+          }
+          return wave_max(mx);
+        };
         // Step j: y = M r~_j (r~_j = beta_j q_j, deferred normalisation), and
         // beta_j^2 = |r~_j|^2, its square root and reciprocal in the same basic
         // block (the reduction overlaps the matvec), then alpha_j and r~_{j+1};
@@ -536,7 +771,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
           const long long ts0 = dbg ? clock64() : 0;
           // beta_j first in program order: its reduction, root and reciprocal
           // depend only on r~_j, so they fill the matvec's latency gaps
-          const double nrm2 = wave_sum(rt0 * rt0 + rt1 * rt1);
+          const double nrm2 = pro ? nrm_c : wave_sum(rt0 * rt0 + rt1 * rt1);
           const double bet = sqrt(nrm2);
           const double ib = 1.0 / bet;
           double my0, my1;   // (M r~_j) = W^1/2 C W^1/2 r~_j
@@ -555,7 +790,10 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
           trw[2 * j + 1] = nrm2;   // every lane stores the same value (no exec-mask branch); T[1] is never used
           tscale = j > 0 ? fmax(tscale, bet) : tscale;
           const bool breakdown = j > 0 && !(bet > 1e-14 * tscale);
-          const bool do_check = j > 0 && (breakdown || j == MMAX || j >= next_check);
+          // with re-orthogonalisation T_nact is exact (the Krylov space of the
+          // active rows is exhausted)
+          const bool exhausted = full && j >= nact;
+          const bool do_check = j > 0 && (breakdown || exhausted || j == MMAX || j >= next_check);
           // Gershgorin bounds of T_j: rows 0 .. j-2 final, row j-1 with beta_{j-1} and beta_j
           const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
           gfin_hi = j > 0 ? fmax(gfin_hi, a_last + b_prev + bet) : gfin_hi;
@@ -569,42 +807,37 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
           double aj = pa * ib * ib;
           double n0 = mq0 - aj * q0 - (j > 0 ? bet * qp0 : 0.0);
           double n1 = mq1 - aj * q1 - (j > 0 ? bet * qp1 : 0.0);
-          if (reorth) {
-            // classical Gram-Schmidt against q_0 .. q_j (read back from the
-            // scratch after the stores landed), a second pass when |r|^2
-            // drops below half (DGKS); alpha takes the q_j coefficients
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const double2* V2 = reinterpret_cast<const double2*>(Vb);
-            double* hb = tb;   // [MMAX + 2] coefficients (the matvec scratch is free until the next step)
-            for (int pass = 0; pass < 2; ++pass) {
-              const int nh = pass == 0 ? j + 2 : j + 1;
-              for (int qq = 0; qq < nh; ++qq) {
-                double v;
-                if (qq <= j) {
-                  const double2 b = V2[qq * 64 + lane];
-                  v = b.x * n0 + b.y * n1;
-                } else {
-                  v = n0 * n0 + n1 * n1;
-                }
-                v = wave_sum(v);
-                if (lane == 0) hb[qq] = v;
+          if (full) gs(j, q0, q1, n0, n1, aj);
+          if (pro) {
+            // partial re-orthogonalisation (Simon): the omega recurrence
+            // estimates q_{j+1} . q_k from T alone; when an estimate passes
+            // sqrt(eps), r~_{j+1} and r~_{j+2} are orthogonalised against the
+            // whole basis and the estimates reset
+            bool did = force;
+            if (force) gs(j, q0, q1, n0, n1, aj);
+            force = false;
+            double nn2 = wave_sum(n0 * n0 + n1 * n1);
+            if (!did) {
+              const double mx = omega_step(j, aj, bet, sqrt(nn2), tscale > fabs(aj) ? tscale : fabs(aj));
+              if (mx > kSqrtEps) {
+                gs(j, q0, q1, n0, n1, aj);
+                nn2 = wave_sum(n0 * n0 + n1 * n1);
+                did = force = true;
               }
-              wsym::lds_order();
-              double up0 = 0.0, up1 = 0.0, hn2 = 0.0;
-              for (int qq = 0; qq <= j; ++qq) {
-                const double hv = hb[qq];
-                const double2 b = V2[qq * 64 + lane];
-                up0 = fma(hv, b.x, up0);
-                up1 = fma(hv, b.y, up1);
-                hn2 = fma(hv, hv, hn2);
-              }
-              n0 -= up0;
-              n1 -= up1;
-              aj += hb[j];
-              const bool again = pass == 0 && hb[j + 1] - hn2 < kDgks * hb[j + 1];
-              wsym::lds_order();
-              if (!again) break;
             }
+            const double bn = sqrt(nn2);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const int k = lane + 64 * s2;
+              al[s2] = k == j ? aj : al[s2];
+              be[s2] = k == j ? bet : be[s2];
+              be1[s2] = k == j ? bn : be1[s2];
+              if (did) {
+                op[s2] = oc[s2];
+                oc[s2] = k <= j ? kEps : (k == j + 1 ? 1.0 : 0.0);
+              }
+            }
+            nrm_c = nn2;
           }
           trw[2 * j] = aj;   // every lane: no exec-mask branch
           if (dbg) tstep += clock64() - ts1;
@@ -624,7 +857,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
             const double res = fabs(bet * zl);
             hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
             theta_lb = lm;
-            if (res <= kAccept * fabs(lm) || breakdown) {
+            if (res <= acc * fabs(lm) || breakdown || exhausted) {
               converged = true;
               m_conv = m;
               lam = lm;
@@ -654,7 +887,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
             double rate = rate_hint;
             if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
             if (rate < 0.0 && res > 0.0) {
-              const double need = log(kAccept * fabs(lm) / res) / rate;
+              const double need = log(acc * fabs(lm) / res) / rate;
               adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
             }
             m_a = m;
@@ -712,7 +945,13 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         }
         u0 = sw0 > 0.0 ? a0 + b0 : 0.0;
         u1 = sw1 > 0.0 ? a1 + b1 : 0.0;
+        if constexpr (MODE == 1) {   // a semi-orthogonal basis (PRO): |V z| = 1 + O(sqrt eps)
+          const double iu = 1.0 / sqrt(wave_sum(u0 * u0 + u1 * u1));
+          u0 *= iu;
+          u1 *= iu;
+        }
       }
+      have_u = true;
       m_hint = m_conv > 8 ? m_conv : 8;
       if (dbg && it < 256) {
         double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
@@ -733,10 +972,18 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
           rec[FNP + 10] = static_cast<double>(tmv);
           rec[FNP + 11] = static_cast<double>(tstep);
           rec[FNP + 12] = trounds;
+          rec[FNP + 15] = ngs;
         }
       }
-      // ---- early exit (robust_estimator.py:163-164)
-      if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
+      // ---- early exit (robust_estimator.py:163-164 / :71-72)
+      if (lam * lam <= A.expansion * A.sigma * A.sigma) {
+        unweighted = none;
+        break;
+      }
+      if (MODE == 1 && none) {
+        if (lane == 0) *A.status = 2;   // c * (1 - step * tau) with c None: TypeError (:75)
+        break;
+      }
       // ---- tau_i = (C W^1/2 u)_i^2 / lambda
       double t0, t1;
       {
@@ -745,10 +992,26 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         wsym::matvec<WKV>(P, cl, zd, tb, z0, z1, t0, t1);
       }
       const double ti0 = t0 * t0 / lam, ti1 = t1 * t1 / lam;
-      // filterL2 (:166-172): c *= 1 - tau / tau_max, the argmax (first index)
-      // removed, c /= |c|_1
-      double tmax = 0.0;
-      {
+      if constexpr (MODE == 1) {
+        // c *= 1 - step tau, then the KL projection onto {sum c = 1, c <= cap}
+        // (robust_estimator.py:74-99) over the n_keep kept clients
+        const double cap = 1.0 / (1.0 - A.eps) / n_keep;
+        if (ai0) ci0 = ci0 * (1.0 - step * ti0);
+        if (ai1) ci1 = ci1 * (1.0 - step * ti1);
+        int capped = 0;
+        if (!wave_kl_project(ci0, ci1, ai0, ai1, n_keep, cap, scr, &capped)) {
+          none = true;   // projected_c = None (:99)
+          unweighted = it + 1 == iters;
+          if (unweighted) {
+            ci0 = ai0 ? 1.0 : ci0;
+            ci1 = ai1 ? 1.0 : ci1;
+          }
+        }
+        if (tr != nullptr && lane == 0) tr[1 + it] = capped;
+      } else {
+        // filterL2 (:166-172): c *= 1 - tau / tau_max, the argmax (first
+        // index) removed, c /= |c|_1
+        double tmax = 0.0;
         const double v0 = ai0 ? ti0 : -__builtin_inf(), v1 = ai1 ? ti1 : -__builtin_inf();
         const bool take1 = v1 > v0;
         const int p = wave_argmax_first(take1 ? v1 : v0, take1 ? r1 : r0, &tmax);
@@ -793,6 +1056,10 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         for (int i = 0; i < n; ++i)
           if (kf[i] != 0.0) kept[q2++] = cv[i];
         A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
+        if constexpr (MODE == 1) {
+          A.misc[static_cast<size_t>(ch) * kMisc + 2] = unweighted ? 1.0 : 0.0;
+          if (unweighted) atomicAdd(A.status + 1, 1);
+        }
       }
       wsym::lds_order();
     }
@@ -802,13 +1069,18 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
 size_t wave_solve_lds() { return kWaveLds; }
 int wave_solve_grid() { return kWaveGrid; }
 
-int launch_wave_solve(bool dbg, const SolveArgs& sa, int grid, hipStream_t s) {
-  const void* k = dbg ? reinterpret_cast<const void*>(&wave_solve_kernel<0, true>)
-                      : reinterpret_cast<const void*>(&wave_solve_kernel<0, false>);
+template <int MODE>
+static int launch_wave_solve_t(bool dbg, const SolveArgs& sa, int grid, hipStream_t s) {
+  const void* k = dbg ? reinterpret_cast<const void*>(&wave_solve_kernel<MODE, true>)
+                      : reinterpret_cast<const void*>(&wave_solve_kernel<MODE, false>);
   SRA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kWaveLds)));
-  if (dbg) hipLaunchKernelGGL((wave_solve_kernel<0, true>), dim3(grid), dim3(64), kWaveLds, s, sa);
-  else hipLaunchKernelGGL((wave_solve_kernel<0, false>), dim3(grid), dim3(64), kWaveLds, s, sa);
+  if (dbg) hipLaunchKernelGGL((wave_solve_kernel<MODE, true>), dim3(grid), dim3(64), kWaveLds, s, sa);
+  else hipLaunchKernelGGL((wave_solve_kernel<MODE, false>), dim3(grid), dim3(64), kWaveLds, s, sa);
   return launch_status("wave_solve_kernel");
+}
+
+int launch_wave_solve(int mode, bool dbg, const SolveArgs& sa, int grid, hipStream_t s) {
+  return mode == 1 ? launch_wave_solve_t<1>(dbg, sa, grid, s) : launch_wave_solve_t<0>(dbg, sa, grid, s);
 }
 
 }  // namespace sra
