@@ -213,17 +213,18 @@ KERNEL_NAME = {
     "trimmedmean": "select_plain_kernel<1, 128, 12>",
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
-    "krum": "whole krum op (bf16x3 gram_partial_kernel dominant; per-kernel split in profiles/)",
+    "krum": "whole krum op (bf16x3 gram_pipe_kernel dominant; per-kernel split in profiles/)",
     "mom_krum": "whole mom_krum op (gram_bucket_kernel: bucket means fused into the bf16x3 Gram + scoring)",
     "bulyankrum": "whole bulyan op (bf16x3 Gram + theta Krum rounds + final stage)",
     "bulyanmedian": "whole bulyan op (theta fused select+distance rounds + final stage)",
     "bulyantrimmedmean": "whole bulyan op (theta fused select+distance rounds + final stage)",
-    "filterl2": "whole filterL2 op (chunk_gram_kernel fp64 MFMA + lanczos_solve_kernel<0>, listed chunks on "
+    "filterl2": "whole filterL2 op (chunk_gram_kernel fp64 MFMA + wave_solve_kernel<0>, listed chunks on "
                 "filter_solve_kernel<0> + chunk_mean_kernel)",
-    "ex_noregret": "whole ex_noregret op (chunk Gram + noregret_pre_kernel + filter_solve_kernel<1> + chunk means)",
-    "mom_filterl2": "whole op (bucket means + chunk Gram + lanczos_solve_kernel<0> / filter_solve_kernel<0> "
-                    "fallback + chunk means)",
-    "mom_ex_noregret": "whole op (bucket means + chunk Gram + filter_solve_kernel<1> + chunk means)",
+    "ex_noregret": "whole ex_noregret op (chunk Gram + noregret_pre_kernel + wave_solve_kernel<1> + chunk means)",
+    "mom_filterl2": "whole op (chunk Gram with the bucket means formed in its loads + wave_solve_kernel<0> / "
+                    "filter_solve_kernel<0> fallback + chunk means)",
+    "mom_ex_noregret": "whole op (chunk Gram with the bucket means formed in its loads + noregret_pre_kernel + "
+                       "wave_solve_kernel<1> + chunk means)",
 }
 
 
@@ -564,7 +565,7 @@ def main():
                  "drift; rows 0..%d Byzantine at -10x the benign mean + 0.001 N(0,1)" % (byz - 1)
                  if byz else "synthetic, generated on device: 0.01 N(0,1) + shared 0.001 N(0,1) drift, no "
                  "Byzantine rows"),
-        "config": {"workload": "%s N=%d clients x d=%.0e fp32 per GPU%s" % (
+        "config": {"workload": "%s N=%d clients x d=%d fp32 per GPU%s" % (
                        a.agg, n, d, ", d-sharded + RCCL all-gather" if world > 1 else ""),
                    "aggregator": a.agg, "clients": n, "d_per_gpu": d, "d_total": d * world,
                    "parallelism": ("block-cyclic d-shard x%d, %d overlapped all-gather rounds" % (world, d // block)

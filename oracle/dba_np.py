@@ -105,8 +105,8 @@ def bulyan_select(X, f, aggsubfunc):
         return selected
     for i in range(theta):
         live = np.array([rows[j] for j in remaining])
-        if aggsubfunc == "median":
-            agg = np.sort(live, axis=0)[(len(remaining) - 1) // 2]
+        if aggsubfunc == "median":   # torch.median: the lower median, NaN propagates (:1038)
+            agg = median(live)
         else:
             b = int((n - i) * 0.1)
             agg = trimmed_mean(live, 0.1) if b > 0 else fed_avg(live)

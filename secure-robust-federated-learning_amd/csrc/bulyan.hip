@@ -87,7 +87,7 @@ template <int P, int MODE>  // MODE: 0 median, 1 trimmed; n in (P-16, P] (P=16: 
 __global__ void __launch_bounds__(256, 3) select_dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
                                                                const int* __restrict__ rows, int nrows_x, int n_arg,
                                                                int64_t d,
-                                                               int lo, int hi, float* __restrict__ out,
+                                                               int lo, int hi, int nan_all, float* __restrict__ out,
                                                                float* __restrict__ bpart, int nb, int tpb) {
   constexpr int P2 = next_pow2(P);
   const unsigned t = threadIdx.x;
@@ -187,7 +187,10 @@ __global__ void __launch_bounds__(256, 3) select_dist_rows_kernel(const float* _
         }
       }
       res = acc_s / static_cast<float>(hi - lo);
-      if (nan_cnt > n - hi) res = qnan();
+      // NaN sorts last (torch.sort / np.sort): the window sees it when it
+      // reaches past n - hi; torch.median (nan_all, the DBA lower median)
+      // propagates any NaN
+      if (nan_cnt > (nan_all ? 0 : n - hi)) res = qnan();
     }
     if (t < rem) out[base + t] = res;
     // step 2: squared distances of the listed rows over this wave's 64 coordinates
@@ -325,7 +328,7 @@ constexpr int kDistRowGroup = 1024;    // dist_rows_kernel<4>: rows per launch a
 __global__ void __launch_bounds__(256) select_rows_lds_kernel(const float* __restrict__ X, int64_t ldx,
                                                               const int* __restrict__ rows, int nrows_x, int n, int pn,
                                                               int tile, int64_t d, int median, int lo, int hi,
-                                                              float* __restrict__ out) {
+                                                              int nan_all, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int64_t j0 = static_cast<int64_t>(blockIdx.x) * tile;
   const int tid = threadIdx.x;
@@ -368,6 +371,7 @@ __global__ void __launch_bounds__(256) select_rows_lds_kernel(const float* __res
         float acc = 0.f;
         for (int p = lo; p < hi; ++p) acc += lds[p * tile + tid];
         res = acc / static_cast<float>(hi - lo);
+        if (nan_all && __builtin_isnan(lds[(n - 1) * tile + tid])) res = qnan();   // torch.median
       }
       out[j] = res;
     }
@@ -1076,7 +1080,7 @@ size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
 
 template <int MODE>
 static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int nrows_x, int n, int64_t d, int lo,
-                              int hi, float* out, float* bpart, hipStream_t s) {
+                              int hi, int nan_all, float* out, float* bpart, hipStream_t s) {
   const int64_t tpb = round_tiles_per_block(d);
   const int64_t blocks = round_blocks(d);
   const int P = static_cast<int>(cdiv(n, 16) * 16);
@@ -1084,7 +1088,7 @@ static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int 
   case PP:                                                                                                     \
     hipLaunchKernelGGL((select_dist_rows_kernel<PP, MODE>), dim3(blocks), dim3(256), 0, s, X, ldx, rows, nrows_x, n,       \
                        d, lo,                                                                                  \
-                       hi, out, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                       \
+                       hi, nan_all, out, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                       \
     return launch_status("select_dist_rows_kernel");
   switch (P) {
     SRA_SR(16) SRA_SR(32) SRA_SR(48) SRA_SR(64) SRA_SR(80) SRA_SR(96) SRA_SR(112) SRA_SR(128)
@@ -1114,7 +1118,9 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows
                          rows, nrows_s, theta, pn, keep, d, out, nf_count, nf_list);
       return launch_status("bulyan_final_lds_kernel");
     };
-    switch (kStageLdsFloats / pn) {
+    // the widest instantiated tile is 64 coordinates (theta in (128, 256]
+    // would allow 128 within the LDS budget)
+    switch (kStageLdsFloats / pn < 64 ? kStageLdsFloats / pn : 64) {
       case 64: rc = run(bulyan_final_lds_kernel<64>, 64); break;
       case 32: rc = run(bulyan_final_lds_kernel<32>, 32); break;
       case 16: rc = run(bulyan_final_lds_kernel<16>, 16); break;
@@ -1158,13 +1164,13 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows
 // shard's share: the shards' dist vectors sum (all-reduce) to the distance
 // over all columns.  bpart: nr x round_blocks(d) floats.
 static int launch_round_big(const float* X, int64_t ldx, const int* rows, int nrows_x, int nr, int64_t d, bool median,
-                            int lo, int hi, float* agg, float* bpart, hipStream_t s) {
+                            int lo, int hi, int nan_all, float* agg, float* bpart, hipStream_t s) {
   SRA_REQUIRE(nr <= kBigMaxClients, SRA_ERR_UNSUPPORTED, "bulyan median/trimmedmean rounds support N <= %d (got %d)",
               kBigMaxClients, nr);
   const int pn = next_pow2(nr);
   const int tile = kBigLdsFloats / pn;
   hipLaunchKernelGGL(select_rows_lds_kernel, dim3(cdiv(d, tile)), dim3(256), sizeof(float) * pn * tile, s, X, ldx,
-                     rows, nrows_x, nr, pn, tile, d, median ? 1 : 0, lo, hi, agg);
+                     rows, nrows_x, nr, pn, tile, d, median ? 1 : 0, lo, hi, nan_all, agg);
   int rc = launch_status("select_rows_lds_kernel");
   if (rc) return rc;
   const int64_t tpb = round_tiles_per_block(d);
@@ -1188,8 +1194,9 @@ static int launch_round_big(const float* X, int64_t ldx, const int* rows, int nr
 
 static int launch_bulyan_round(const float* X, int nrows_x, int64_t d, int64_t ldx, const int* rows, int nr, int mode,
                                bool dba, float* agg, float* bpart, double* dist, hipStream_t s) {
-  int lo, hi, sel_mode;
+  int lo, hi, sel_mode, nan_all = 0;
   if (mode == kBulyanMedian && dba) {
+    nan_all = 1;         // torch.median propagates NaN (helper.py:1038 -> the assert at :1047)
     lo = (nr - 1) / 2;   // torch.median: s[(n-1)//2]
     hi = lo + 1;
     sel_mode = 1;
@@ -1205,11 +1212,11 @@ static int launch_bulyan_round(const float* X, int nrows_x, int64_t d, int64_t l
   }
   int rc;
   if (nr > 128)
-    rc = launch_round_big(X, ldx, rows, nrows_x, nr, d, sel_mode == 0, lo, hi, agg, bpart, s);
+    rc = launch_round_big(X, ldx, rows, nrows_x, nr, d, sel_mode == 0, lo, hi, nan_all, agg, bpart, s);
   else if (sel_mode == 0)
-    rc = launch_select_dist<0>(X, ldx, rows, nrows_x, nr, d, lo, hi, agg, bpart, s);
+    rc = launch_select_dist<0>(X, ldx, rows, nrows_x, nr, d, lo, hi, nan_all, agg, bpart, s);
   else
-    rc = launch_select_dist<1>(X, ldx, rows, nrows_x, nr, d, lo, hi, agg, bpart, s);
+    rc = launch_select_dist<1>(X, ldx, rows, nrows_x, nr, d, lo, hi, nan_all, agg, bpart, s);
   if (rc) return rc;
   hipLaunchKernelGGL(bulyan_dist_reduce_kernel, dim3(nr), dim3(256), 0, s, bpart, static_cast<int>(round_blocks(d)),
                      dist);

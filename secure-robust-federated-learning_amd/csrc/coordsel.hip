@@ -360,7 +360,7 @@ __device__ __forceinline__ float from_lane(float x) {
 // NT: streaming (non-temporal) row loads.  A wave's load instruction covers
 // 16 coordinates = half a 128-byte line per row, the other half belongs to
 // the neighbouring wave of the block, so the N = 512 launches use plain loads
-// (SRA_QUAD_NT=1 restores streaming loads for A/B runs).
+// (the NT template parameter picks the load kind per instantiation).
 template <int L, int MODE, int NX = 0, int BX = -1, bool NT = true>
 __global__ void __launch_bounds__(256) select_quad_kernel(const float* __restrict__ X, int n_rt, int64_t d,
                                                          int64_t ldx, int lo_rt, int hi_rt, float* __restrict__ out) {

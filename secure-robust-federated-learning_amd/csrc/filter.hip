@@ -2051,7 +2051,12 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
   const int* ab = act + static_cast<size_t>(b) * cs;
   if (unw && misc[static_cast<size_t>(b) * kMisc + 2] != 0.0) {
     // ex_noregret's np.average(samples, weights=None) of fp32 samples: the
-    // sequential fp32 sum over the kept clients / their count, in fp32
+    // sequential fp32 sum over the kept clients / their count, in fp32.
+    // Deviation: the sum runs in client-index order; the reference's kept
+    // list is in np.argpartition's order (robust_estimator.py:49-50, an
+    // introselect detail of numpy), so the two fp32 sums can differ in the
+    // last ulps (the unweighted outcome itself only exists in the fp32
+    // window of tests/golden/gen_none_sides.py; the tests bound it by tolerance)
     float s32 = 0.f;
     int cnt = 0;
     for (int i = 0; i < n; ++i)

@@ -235,9 +235,12 @@ class HelperAggregation:
         if st.n - 2 * f <= 0:
             raise RuntimeError("torch.cat(): expected a non-empty list of Tensors")   # helper.py:985 / 1035
         chosen = {}
+        status = torch.zeros(len(st.keys), dtype=torch.int32, device=st.X.device)
         for l, k in enumerate(st.keys):
-            out = engine.bulyan_dba(st.cols(l), f, mode)
+            out = engine.bulyan_dba(st.cols(l), f, mode, status=status[l:l + 1])
             chosen[k] = out.float().reshape(st.shapes[l])
+        if mode != "krum":   # helper.py:1047 / :1119, one read back per round
+            engine.check_bulyan_status(status, "bulyan_dba(%s)" % mode)
         self._apply(target_model, chosen)
         return True
 

@@ -175,8 +175,11 @@ def _device_round(agg, st, args, state, local_grads, choices):
         return out, None
     if agg in _BULYAN:
         out = torch.empty(seg[-1], dtype=torch.float64, device=X.device)
+        status = torch.zeros(st.nlayers, dtype=torch.int32, device=X.device)
         for l in range(st.nlayers):
-            out[seg[l]:seg[l + 1]] = engine.bulyan(st.cols(l), f, _BULYAN[agg])
+            out[seg[l]:seg[l + 1]] = engine.bulyan(st.cols(l), f, _BULYAN[agg], status=status[l:l + 1])
+        if agg != "bulyankrum":   # one read back per round (robust_estimator.py:308, 321)
+            engine.check_bulyan_status(status, "bulyan(%s)" % _BULYAN[agg])
         return out, None
     if agg in ("filterl2", "ex_noregret", "mom_filterl2", "mom_ex_noregret"):
         src = X

@@ -212,13 +212,16 @@ def mom_krum(X, f, bucket_size=3, fused=True):
 BULYAN_MODES = {"krum": 0, "median": 1, "trimmedmean": 2}
 
 
-def bulyan(X, f, aggsubfunc="trimmedmean", selected=False, check=True):
+def bulyan(X, f, aggsubfunc="trimmedmean", selected=False, check=True, status=None):
     """robust_estimator.bulyan on device: float64 (d,) aggregate.
     With selected=True also returns the theta chosen clients (krum mode).
     check=True reads the selection status back (one host synchronisation) and
     raises AssertionError where the reference's ``assert min_index != None``
     fails (robust_estimator.py:308, 321): a median / trimmed-mean round whose
-    distances are all NaN / inf, e.g. bulyan(..., 'median') with a NaN client."""
+    distances are all NaN / inf, e.g. bulyan(..., 'median') with a NaN client.
+    Krum mode has no such assert and never reads back.  status: a device int32
+    slot to write the status into instead (no read back: a caller running
+    several layers checks them once with check_bulyan_status)."""
     X, n, d, ldx = as_matrix(X)
     if aggsubfunc not in BULYAN_MODES:
         raise ValueError("aggsubfunc must be one of %s" % sorted(BULYAN_MODES))
@@ -226,16 +229,23 @@ def bulyan(X, f, aggsubfunc="trimmedmean", selected=False, check=True):
     theta = n - 2 * int(f)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
     sel = torch.empty(max(theta, 1), dtype=torch.int32, device=X.device) if selected else None
-    status = torch.empty(1, dtype=torch.int32, device=X.device)
+    own = status is None
+    if own:
+        status = torch.empty(1, dtype=torch.int32, device=X.device)
     nb = _lib.query_bytes("sra_bulyan_workspace_bytes", n, d, int(f), mode)
     ws = _workspace(nb, X.device)
     _lib.call("sra_bulyan_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
               sel.data_ptr() if sel is not None else None, status.data_ptr(), ws.data_ptr(), nb,
               _stream_ptr(X.device))
-    if check and int(status.item()) == 1:
-        raise AssertionError("bulyan(%s): a selection round found no finite distance (min_index is None)"
-                             % aggsubfunc)
+    if own and check and mode != 0:
+        check_bulyan_status(status, "bulyan(%s)" % aggsubfunc)
     return (out, sel) if selected else out
+
+
+def check_bulyan_status(status, what="bulyan"):
+    """One read back of the status slots of one or more Bulyan calls."""
+    if int(status.max().item()) == 1:
+        raise AssertionError("%s: a selection round found no finite distance (min_index is None)" % what)
 
 
 def bulyan_round(X, rows, nr, aggsubfunc, agg, dist, dba=False):
@@ -563,16 +573,27 @@ def weighted_sum(X, w, out=None):
     return out
 
 
-def bulyan_dba(X, f, aggsubfunc="trimmedmean", selected=False):
+def bulyan_dba(X, f, aggsubfunc="trimmedmean", selected=False, check=True, status=None):
     """Helper.bulyan_krum / bulyan_median / bulyan_trimmed_mean selection rules
-    (helper.py:942-1137) with the shared per-coordinate stage; float64 (d,)."""
+    (helper.py:942-1137) with the shared per-coordinate stage; float64 (d,).
+    check=True raises AssertionError where helper.py's ``assert min_index !=
+    None`` fails (:1047, :1119): a round whose distances are all NaN / inf.
+    status: as for bulyan()."""
     X, n, d, ldx = as_matrix(X)
+    if aggsubfunc not in BULYAN_MODES:
+        raise ValueError("aggsubfunc must be one of %s" % sorted(BULYAN_MODES))
     mode = BULYAN_MODES[aggsubfunc]
     theta = n - 2 * int(f)
     out = torch.empty(d, dtype=torch.float64, device=X.device)
     sel = torch.empty(max(theta, 1), dtype=torch.int32, device=X.device) if selected else None
+    own = status is None
+    if own:
+        status = torch.empty(1, dtype=torch.int32, device=X.device)
     nb = _lib.query_bytes("sra_bulyan_workspace_bytes", n, d, int(f), mode)
     ws = _workspace(nb, X.device)
     _lib.call("sra_bulyan_dba_f32", X.data_ptr(), n, d, ldx, int(f), mode, out.data_ptr(),
-              sel.data_ptr() if sel is not None else None, None, ws.data_ptr(), nb, _stream_ptr(X.device))
+              sel.data_ptr() if sel is not None else None, status.data_ptr(), ws.data_ptr(), nb,
+              _stream_ptr(X.device))
+    if own and check and mode != 0:
+        check_bulyan_status(status, "bulyan_dba(%s)" % aggsubfunc)
     return (out, sel) if selected else out

@@ -143,7 +143,15 @@ def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
 
     gram_fn(X_shard) -> (N, N) float64 partial centred Gram;
     select_fn(G, f) -> index of the chosen client (from the full Gram).
-    Returns (full row of the chosen client, index)."""
+    Returns (full row of the chosen client, index).
+
+    Deviation from the single-GPU engine.krum: sra_krum_select_f32 re-derives
+    the distances of near-tied or non-finite pairs exactly from the rows (the
+    Gram's |a|^2 + |b|^2 - 2ab cancels there, and inf - inf is NaN); a
+    sharded layer's rows are split over the ranks, so the pick here always
+    comes from the summed Gram.  Finite, well-separated data pick the same
+    client (tests/test_gpu_shard2.py); ties within the Gram's rounding and
+    inf entries can pick differently than the reference."""
     G = gram_fn(X_shard).to(torch.float64).contiguous()
     # (a 1-rank group still goes through the collectives)
     idx = int(_gram_pick(G, lambda g: torch.tensor([int(select_fn(g, f))]), 1, group)[0])

@@ -55,6 +55,11 @@ CASES = {
     "bulyanmedian_n30_f8_negbeta": ("bulyan_median", {"f": 8}, 30, 8, {}, 1),
     "bulyantrimmed_n40_f12_negbeta": ("bulyan_trimmed_mean", {"f": 12}, 40, 12, {}, 1),
     "bulyanmedian_n30_f10_negbeta": ("bulyan_median", {"f": 10}, 30, 10, {}, 1),
+    # a NaN coordinate in one client (case_rows injects it): torch.median propagates it, every distance
+    # of the round is NaN and ``assert min_index != None`` fails (helper.py:1047 / :1119)
+    "bulyanmedian_nan_n24_f5": ("bulyan_median", {"f": 5}, 24, 5, {}, 1),
+    "bulyantrimmed_nan_n24_f5": ("bulyan_trimmed_mean", {"f": 5}, 24, 5, {}, 1),
+    "bulyankrum_nan_n24_f5": ("bulyan_krum", {"f": 5}, 24, 5, {}, 1),
 }
 
 BASE_PARAMS = {"eta": 1, "sharding": False, "shard_size": 0.2, "adversary_list": [0, 1, 2, 3, 4],
@@ -67,6 +72,8 @@ def case_rows(name, rnd=0):
     _, _, n, byz, _, _ = CASES[name]
     seed = 1000 + 97 * list(CASES).index(name) + rnd
     x = make_rows(n, D, seed, byz=byz)
+    if "_nan_" in name:
+        x[7, 13] = np.nan
     ns = np.random.default_rng(seed + 1).integers(200, 600, size=n).astype(np.int64)
     return x, ns
 

@@ -60,18 +60,31 @@ def _near(cand, ref, atol, rtol):
 @pytest.mark.parametrize("name", ["bulyankrum_n24_f5", "bulyankrum_n25_f2", "bulyanmedian_n25_f5",
                                   "bulyanmedian_n24_f5", "bulyantrimmed_n25_f5", "bulyankrum_n30_f8_negbeta",
                                   "bulyanmedian_n30_f8_negbeta", "bulyantrimmed_n40_f12_negbeta",
-                                  "bulyanmedian_n30_f10_negbeta"])
+                                  "bulyanmedian_n30_f10_negbeta", "bulyantrimmed_nan_n24_f5",
+                                  "bulyankrum_nan_n24_f5"])
 def test_bulyan_one_of_two_medians(name):
     method, kw, *_ = CASES[name]
     mode = {"bulyan_krum": "krum", "bulyan_median": "median", "bulyan_trimmed_mean": "trimmedmean"}[method]
     x, _ = case_rows(name)
     cand = od.bulyan_candidates(x, SEG, kw["f"], mode)
     ref = fx(name)["out_0"].astype(np.float64)
-    ok = _near(cand, ref, 1e-7, 2e-6)
+    got = od.bulyan(x, SEG, kw["f"], mode)
+    # NaN client picked first by Krum (helper.py:982): NaN in the reference and the oracle alike
+    nan_pick = np.isnan(ref) & np.isnan(got)
+    assert np.array_equal(np.isnan(ref), np.isnan(got))
+    ok = _near(cand, ref, 1e-7, 2e-6) | nan_pick
     assert ok.all(), np.nonzero(~ok)
     # the shared fp64 stage lands on one of the candidates too
-    got = od.bulyan(x, SEG, kw["f"], mode)
-    assert _near(cand, got, 1e-12, 1e-12).all()
+    assert (_near(cand, got, 1e-12, 1e-12) | nan_pick).all()
+
+
+def test_bulyan_median_nan_asserts():
+    """helper.py:1047: a NaN coordinate propagates through torch.median; no
+    finite distance, ``assert min_index != None`` fails in the reference and the oracle."""
+    assert str(fx("bulyanmedian_nan_n24_f5")["error"]) == "AssertionError"
+    x, _ = case_rows("bulyanmedian_nan_n24_f5")
+    with pytest.raises(AssertionError):
+        od.bulyan(x, SEG, 5, "median")
 
 
 def test_filterl2():

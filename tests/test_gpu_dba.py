@@ -112,7 +112,8 @@ def _near(cand, ref, atol, rtol):
 @pytest.mark.parametrize("name", ["bulyankrum_n24_f5", "bulyankrum_n25_f2", "bulyanmedian_n25_f5",
                                   "bulyanmedian_n24_f5", "bulyantrimmed_n25_f5", "bulyankrum_n30_f8_negbeta",
                                   "bulyanmedian_n30_f8_negbeta", "bulyantrimmed_n40_f12_negbeta",
-                                  "bulyanmedian_n30_f10_negbeta"])
+                                  "bulyanmedian_n30_f10_negbeta", "bulyantrimmed_nan_n24_f5",
+                                  "bulyankrum_nan_n24_f5"])
 def test_bulyan(name):
     method, kw, *_ = CASES[name]
     mode = {"bulyan_krum": "krum", "bulyan_median": "median", "bulyan_trimmed_mean": "trimmedmean"}[method]
@@ -122,8 +123,23 @@ def test_bulyan(name):
     np.testing.assert_allclose(got, od.bulyan(x, SEG, kw["f"], mode).astype(np.float32), rtol=0, atol=0)
     cand = od.bulyan_candidates(x, SEG, kw["f"], mode)
     ref = fx(name)["out_0"].astype(np.float64)
-    assert _near(cand, ref, 1e-7, 2e-6).all()
-    assert _near(cand, got.astype(np.float64), 1e-7, 2e-6).all()
+    # a NaN client Krum picks first (np.argmin of a NaN score, helper.py:982) puts NaN among each of its
+    # coordinates' selected values: NaN there in the reference and on the device (the candidates skip it)
+    nan_pick = np.isnan(ref) & np.isnan(got)
+    assert np.array_equal(np.isnan(ref), np.isnan(got))
+    assert (_near(cand, ref, 1e-7, 2e-6) | nan_pick).all()
+    assert (_near(cand, got.astype(np.float64), 1e-7, 2e-6) | nan_pick).all()
+
+
+def test_bulyan_median_nan_raises():
+    """helper.py:1047: torch.median propagates the NaN client's coordinate, every
+    distance of the round is NaN, ``assert min_index != None`` fails."""
+    assert str(fx("bulyanmedian_nan_n24_f5")["error"]) == "AssertionError"
+    with pytest.raises(AssertionError):
+        _run("bulyanmedian_nan_n24_f5")
+    x, _ = case_rows("bulyanmedian_nan_n24_f5")
+    with pytest.raises(AssertionError):
+        od.bulyan(x, SEG, 5, "median")
 
 
 def test_bulyan_krum_f1_rejected_and_theta():
