@@ -400,6 +400,10 @@ __global__ void __launch_bounds__(256) gram_reduce2_kernel(const double* __restr
   const int i = 32 * C::kTileI(tile) + (el >> 5);
   const int j = 32 * C::kTileJ(tile) + (el & 31);
   if (i >= n || j >= n) return;
+  // a diagonal tile holds both (i, j) and (j, i), whose MFMA sums may differ in
+  // the last bits: only the upper one writes the pair (two writers of one
+  // address made G differ from call to call)
+  if (C::kTileI(tile) == C::kTileJ(tile) && (el >> 5) > (el & 31)) return;
   double s = 0.0;
 #pragma unroll 8
   for (int g = 0; g < kRedGroups; ++g) s += partial[static_cast<int64_t>(g) * C::T * 1024 + e];
@@ -424,6 +428,7 @@ __global__ void __launch_bounds__(256) gram_reduce2_pair_kernel(const double* __
   if (i >= n || j >= n) return;
   const bool ia = i < split, ja = j < split;
   if ((ia && ja && !write_aa) || (!ia && !ja && !write_bb)) return;
+  if (C::kTileI(tile) == C::kTileJ(tile) && (el >> 5) > (el & 31)) return;   // as gram_reduce2_kernel
   double s = 0.0;
 #pragma unroll 8
   for (int g = 0; g < kRedGroups; ++g) s += partial[static_cast<int64_t>(g) * C::T * 1024 + e];

@@ -138,3 +138,31 @@ def test_oracle_bulyan_scalar_helpers():
                 continue
             assert got == one or abs(got - one) <= 1e-15 * max(1.0, abs(one)) or (np.isnan(got) and np.isnan(one))
     assert n_tie > 0
+
+
+def test_projection_infeasible_only_when_cap_reaches_one():
+    """robust_estimator.py:78-99: let I be the last candidate with clip_I =
+    1 - (I+1) cap > 0.  Then clip_{I+1} <= 0 gives clip_I <= cap, and the
+    rescaled largest remaining weight is c_max clip_I / S_rest <= clip_I <= cap:
+    candidate I always passes the :92 test.  So projected_c is None exactly when
+    no candidate has clip > 0, i.e. cap = 1 / ((1 - eps) n') >= 1 -- fixed for
+    the chunk, so the None happens at iteration 0 or never, and the unweighted
+    iteration after it sees iteration 0's covariance (in fp32).  This is why the
+    None-then-exit outcome only exists inside the fp32 window that
+    ex_noregret_none_below / ex_noregret_exit_above bracket (DESIGN.md
+    section 4).  Checked here on weights spread over 12 orders of magnitude."""
+    import warnings
+    from oracle import robust_np as orc
+    rng = np.random.default_rng(7)
+    warnings.simplefilter("ignore")
+    for _ in range(3000):
+        n = int(rng.integers(2, 40))
+        eps = float(rng.uniform(0.0, 0.6))
+        c = np.exp(rng.uniform(-28.0, 0.0, n)) * (rng.uniform() if rng.uniform() < 0.5 else 1.0)
+        got = orc.kl_capped_projection(c, eps)
+        cap = 1.0 / (1 - eps) / n
+        if cap < 1.0 - 1e-12:
+            assert got is not None, (n, eps)
+            assert got.max() <= cap * (1 + 1e-12) and abs(got.sum() - 1.0) < 1e-9
+        elif cap >= 1.0:
+            assert got is None
