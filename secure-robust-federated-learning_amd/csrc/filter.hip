@@ -18,26 +18,22 @@
 //                       distances from G, numpy pairwise score sums, the
 //                       ceil(eps*n) largest scores dropped) and the step size
 //                       0.5 / max pairwise distance^2 in fp32.
-//   filter_solve_kernel the iterations, one 256-thread workgroup per chunk
-//                       (two per CU), G resident in registers (a row per lane
-//                       pair).  Per iteration, with w = c / sum(c):
-//                         C = G - g 1^T - 1 g^T + s 1 1^T (g = G w, s = w^T G w)
-//                         is the Gram of x_i - mu, so the covariance's nonzero
-//                         spectrum is that of M = W^1/2 C W^1/2;
-//                         top eigenpair (lambda, u) of M by Lanczos with full
-//                         re-orthogonalisation (classical Gram-Schmidt, a second
-//                         pass only under heavy cancellation) and deferred
-//                         normalisation: three barriers per step; the
-//                         tridiagonal's top eigenpair (multisection on Sturm
-//                         counts, eigenvector from the bottom pivots) only at
-//                         predicted convergence points, computed redundantly by
-//                         every wave (no extra barrier);
-//                         tau_j = ((x_j - mu).v)^2 = (C W^1/2 u)_j^2 / lambda;
-//                         early exit if lambda^2 <= expansion * sigma^2;
-//                         filterL2: c *= 1 - tau/tau_max, drop argmax, c /= |c|_1;
-//                         ex_noregret: c *= 1 - step*tau, KL projection onto the
-//                         capped simplex (every candidate evaluated in parallel,
-//                         numpy's pairwise fp64 sums emulated).
+//   wave_solve_kernel   (filter_wave.hip, round 5) the iterations, ONE wave
+//                       per chunk, four per CU, C packed in the wave's
+//                       registers and LDS and recentred in place; per
+//                       iteration with w = c / sum(c), the covariance's
+//                       nonzero spectrum is that of M = W^1/2 C W^1/2; top
+//                       eigenpair (lambda, u) by Lanczos (plain for filterL2,
+//                       partial re-orthogonalisation for ex_noregret) with
+//                       checks at predicted convergence points;
+//                       tau_j = (C W^1/2 u)_j^2 / lambda; early exit if
+//                       lambda^2 <= expansion * sigma^2; filterL2:
+//                       c *= 1 - tau/tau_max, drop argmax, c /= |c|_1;
+//                       ex_noregret: c *= 1 - step*tau, KL projection onto the
+//                       capped simplex.
+//   filter_solve_kernel the rare chunk the one-wave solver lists (ghost after
+//                       the retries): one 256-thread workgroup per chunk, G in
+//                       registers, full re-orthogonalisation.
 //   chunk_mean_kernel   mu_j = sum_i c_i x_ij / sum_i c_i in fp64 over the kept
 //                       clients in client order (the reference's np.average),
 //                       one lane per coordinate; HBM bound.
@@ -564,7 +560,7 @@ __device__ __forceinline__ bool kl_project(double* ci_io, bool ai, int row, bool
 
 // MODE 0: filterL2, 1: ex_noregret; DBG: diagnostics of chunk 0.  Since round
 // 2 this re-orthogonalising solver is the fallback: it runs only the chunks
-// that lanczos_solve_kernel listed in A.fb_list (A.fb_count on the device).
+// that wave_solve_kernel listed in A.fb_list (A.fb_count on the device).
 template <int MODE, bool DBG>
 __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -994,1044 +990,9 @@ __global__ void __launch_bounds__(256, 2) filter_solve_kernel(SolveArgs A) {
   }
 }
 
-// ============================================================================
-// lanczos_solve_kernel: the filter iterations with plain Lanczos
-// ============================================================================
-// Each iteration's top eigenvector is essentially new (the filter just damped
-// the previous top direction: consecutive eigenvectors overlap ~0.1 on the
-// bench data), so every iteration runs ~50-90 Lanczos steps from scratch.
-// Plain three-term Lanczos stopped within a few steps of convergence gives the
-// top Ritz pair to ~3e-15 (modelled in numpy against LAPACK; Paige: the loss
-// of orthogonality only sets in along a Ritz vector once it has converged),
-// so this solver keeps no basis on chip and does no re-orthogonalisation:
-// two block reductions per step (alpha; |r|^2 with the centring sums of the
-// next vector), the basis vectors go to a per-workgroup global scratch (L2)
-// for the Ritz vector, and the LDS per chunk drops from 80 KiB to ~22 KiB.
-// Checks run at most kMaxAdvance steps apart once a first check has measured
-// the residual decay, so a check never lands after a ghost copy of the top
-// Ritz value has formed (~15-20 steps after convergence).  A chunk that has
-// not converged after MMAX steps, or whose residual grows between checks (a
-// ghost) after a dense-check retry, takes a third, re-orthogonalising attempt
-// in the same kernel (classical Gram-Schmidt + DGKS against the stored basis).
-
-// Top Ritz pair of T_m (m <= MMAX), block-wide (all four waves call it):
-//   1. its eigenvalue by multisection on Sturm counts over 256 points (64 per
-//      wave; the division-free recurrence P_k = (alpha_k - x) P_{k-1} -
-//      beta^2 P_{k-2} with (alpha, beta^2) pairs broadcast from LDS, one
-//      barrier per round).  theta_lb (the previous check's Ritz value, a lower
-//      bound by interlacing) and hint (its last increase) give a first bracket
-//      a few ulps to a few 1e-10 wide; without them the first round is
-//      geometric above max(alpha_0, theta_lb);
-//   2. the forward pivots dp_q on wave 0 and the backward pivots dm_q on wave 1
-//      at the same time (serial chains on register-resident T, readlane);
-//   3. wave 0: the twist (smallest |gamma_q|), the product walks, the
-//      normalised eigenvector into z[0, m).
-// Record layout: T[2q] = alpha_q, T[2q+1] = beta^2 of (q-1, q).  The residual
-// of the pair is beta_m |z_{m-1}| (returned in *zlast_out): the last component
-// must come from the twisted factorisation -- P_{m-1}(theta) / P_m'(theta)
-// has a ~1e-16 floor once consecutive Ritz values agree to the last ulp.
-// scr: >= 2 * MMAX + 16 doubles of LDS.
-__device__ __attribute__((noinline)) void block_check(const double* T, int m, double theta_lb, double hint,
-                                                      double tscale, double* z, double* scr, double* theta_out,
-                                                      double* zlast_out, int* rounds_out) {
-  m = __builtin_amdgcn_readfirstlane(m);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double2* T2 = reinterpret_cast<const double2*>(T);
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(scr + 2 * MMAX);   // [2][4]
-  double* res = scr + 2 * MMAX + 8;                                                    // [4] results
-  // Gershgorin bounds (every wave, identical)
-  double glo = 1e300, ghi = -1e300;
-  for (int q = lane; q < m; q += 64) {
-    const double r = (q >= 1 ? sqrt(T[2 * q + 1]) : 0.0) + (q + 1 < m ? sqrt(T[2 * q + 3]) : 0.0);
-    glo = fmin(glo, T[2 * q] - r);
-    ghi = fmax(ghi, T[2 * q] + r);
-  }
-  glo = wave_min(glo);
-  ghi = wave_max(ghi);
-  const double a0 = T[0];
-  double lo = fmax(glo, fmax(theta_lb, a0));
-  double hi = ghi;
-  if (!(lo < hi)) lo = glo;
-  const bool hinted = hint >= 0.0 && theta_lb > -1e299;
-  const double hg = lo + 4.0 * hint + 4e-16 * fabs(lo);
-  auto count = [&](double x) -> int {
-    double p2 = 1.0, p1 = a0 - x;
-    unsigned cnt = static_cast<unsigned>(__builtin_bit_cast(unsigned long long, p1) >> 63);
-    auto step = [&](double2 t) __attribute__((always_inline)) {
-      const double pk = fma(t.x - x, p1, -(t.y * p2));
-      cnt += static_cast<unsigned>((__builtin_bit_cast(unsigned long long, pk) ^
-                                    __builtin_bit_cast(unsigned long long, p1)) >> 63);
-      p2 = p1;
-      p1 = pk;
-    };
-    int q = 1;
-    for (; q + 4 <= m; q += 4) {
-      const double2 t0 = T2[q], t1 = T2[q + 1], t2 = T2[q + 2], t3 = T2[q + 3];
-      step(t0);
-      step(t1);
-      step(t2);
-      step(t3);
-      const int e = __builtin_amdgcn_frexp_exp(p1);
-      p1 = __builtin_amdgcn_ldexp(p1, -e);
-      p2 = __builtin_amdgcn_ldexp(p2, -e);
-    }
-    for (; q < m; ++q) step(T2[q]);
-    return static_cast<int>(cnt);
-  };
-  int round = 0;
-  for (; round < 24; ++round) {
-    // point p of this round (identical formula in every lane)
-    const int kind = round == 0 ? (hinted && hg < hi ? 1 : 2) : 0;
-    const double rlo = lo, rhi = hi;
-    auto point = [&](int p) -> double {
-      if (kind == 1) return p < 255 ? rlo + (hg - rlo) * ((p + 1) * (1.0 / 255.0)) : rhi;
-      if (kind == 2) return rlo + (rhi - rlo) * __builtin_amdgcn_ldexp(1.0, p - 255);
-      return rlo + (rhi - rlo) * ((p + 1) * (1.0 / 257.0));
-    };
-    const unsigned long long ok = __builtin_amdgcn_ballot_w64(count(point(64 * wave + lane)) >= m);
-    unsigned long long* M = masks + 4 * (round & 1);
-    if (lane == 0) M[wave] = ok;
-    __syncthreads();
-    int first = 256;
-    for (int w = 3; w >= 0; --w)
-      if (M[w]) first = 64 * w + __builtin_ctzll(M[w]);
-    const double xf = first < 256 ? point(first) : rhi;
-    const double xb = first > 0 ? point(first - 1) : rlo;
-    const bool stalled = xb == lo && xf == hi;
-    lo = xb;
-    hi = xf;
-    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
-  }
-  const double lm = 0.5 * (lo + hi);
-  // ---- pivots: forward on wave 0, backward on wave 1
-  const double tiny = 1e-300 + 1e-30 * tscale;
-  double al[2], b2[2], bl[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int q = lane + 64 * s;
-    al[s] = q < m ? T[2 * q] : 0.0;
-    b2[s] = q + 1 < m ? T[2 * q + 3] : 0.0;
-    bl[s] = sqrt(b2[s]);
-  }
-  double* dps = scr;          // [MMAX] forward pivots
-  double* dms = scr + MMAX;   // [MMAX] backward pivots
-  const int e0 = m < 64 ? m : 64;
-  if (wave == 0) {
-    double dp[2] = {0.0, 0.0};
-    double pf = 0.0;
-    auto fwd = [&](auto S, int q) __attribute__((always_inline)) {
-      constexpr int s = decltype(S)::value;
-      double v = readlane_f64(al[s], q & 63) - lm;
-      if (q > 0) v -= fdiv(s == 0 || q > 64 ? readlane_f64(b2[s], (q - 1) & 63) : readlane_f64(b2[0], 63), pf);
-      if (fabs(v) < tiny) v = -tiny;
-      pf = v;
-      dp[s] = lane == (q & 63) ? v : dp[s];
-    };
-    for (int q = 0; q < e0; ++q) fwd(std::integral_constant<int, 0>{}, q);
-    for (int q = 64; q < m; ++q) fwd(std::integral_constant<int, 1>{}, q);
-    dps[lane] = dp[0];
-    dps[lane + 64] = dp[1];
-  } else if (wave == 1) {
-    double dm[2] = {0.0, 0.0};
-    double pb = 0.0;
-    auto bwd = [&](auto S, int q) __attribute__((always_inline)) {
-      constexpr int s = decltype(S)::value;
-      double v = readlane_f64(al[s], q & 63) - lm;
-      if (q < m - 1) v -= fdiv(readlane_f64(b2[s], q & 63), pb);
-      if (fabs(v) < tiny) v = -tiny;
-      pb = v;
-      dm[s] = lane == (q & 63) ? v : dm[s];
-    };
-    for (int q = m - 1; q >= 64; --q) bwd(std::integral_constant<int, 1>{}, q);
-    for (int q = e0 - 1; q >= 0; --q) bwd(std::integral_constant<int, 0>{}, q);
-    dms[lane] = dm[0];
-    dms[lane + 64] = dm[1];
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const double dp[2] = {dps[lane], dps[lane + 64]};
-    const double dm[2] = {dms[lane], dms[lane + 64]};
-    const double dmn[2] = {dms[lane + 1], lane + 65 < MMAX ? dms[lane + 65] : 0.0};
-    double gam = 1e308;
-    int tw = 0;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int q = lane + 64 * s;
-      const double gq = q < m ? fabs(dp[s] + dm[s] - (al[s] - lm)) : 1e308;
-      if (gq < gam) {
-        gam = gq;
-        tw = q;
-      }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const double og = __shfl_xor(gam, off);
-      const int ot = __shfl_xor(tw, off);
-      if (og < gam || (og == gam && ot < tw)) {
-        gam = og;
-        tw = ot;
-      }
-    }
-    tw = __builtin_amdgcn_readfirstlane(tw);
-    // q < tw: z_q = -(b_q / dp_q) z_{q+1};  q >= tw: z_{q+1} = -(b_q / dm_{q+1}) z_q
-    double rat[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int q = lane + 64 * s;
-      rat[s] = q < tw ? -bl[s] / dp[s] : (q + 1 < m ? -bl[s] / dmn[s] : 0.0);
-    }
-    double zv[2] = {lane == tw ? 1.0 : 0.0, lane + 64 == tw ? 1.0 : 0.0};
-    {
-      double zd = 1.0, zu = 1.0;
-      const int sd = tw, su = m - 1 - tw;
-      const int steps = sd > su ? sd : su;
-      for (int k = 0; k < steps; ++k) {
-        if (k < sd) {
-          const int q = tw - 1 - k;
-          zd *= rl_any(rat, q);
-          if (fabs(zd) > 1e150) zd = copysign(1e150, zd);
-          if (q < 64) zv[0] = lane == q ? zd : zv[0];
-          else zv[1] = lane == q - 64 ? zd : zv[1];
-        }
-        if (k < su) {
-          const int q = tw + k;
-          zu *= rl_any(rat, q);
-          if (fabs(zu) > 1e150) zu = copysign(1e150, zu);
-          if (q + 1 < 64) zv[0] = lane == q + 1 ? zu : zv[0];
-          else zv[1] = lane == q + 1 - 64 ? zu : zv[1];
-        }
-      }
-    }
-    const double amax = wave_max(fmax(fabs(zv[0]), fabs(zv[1])));
-    const double zs0 = zv[0] / amax, zs1 = zv[1] / amax;
-    const double inv = 1.0 / sqrt(wave_sum(zs0 * zs0 + zs1 * zs1));
-    if (lane < m) z[lane] = zs0 * inv;
-    if (lane + 64 < m) z[lane + 64] = zs1 * inv;
-    const double zl = rl_any(zv, m - 1) / amax * inv;
-    if (lane == 0) {
-      res[0] = lm;
-      res[1] = zl;
-    }
-  }
-  __syncthreads();
-  *theta_out = res[0];
-  *zlast_out = res[1];
-  *rounds_out = round + 1;
-}
-
-// Top Ritz pair of T_m, block-wide, tuned for latency (round 3; replaces
-// block_check in the solver).  T_m's coefficients are loaded once into
-// registers (lane q holds alpha_q, beta^2_{q-1}, beta^2_q for q = lane and
-// lane + 64) and every serial chain takes them by v_readlane (no LDS latency
-// on a chain); the Gershgorin bounds [glo, ghi] are kept by the caller.
-//   1. the eigenvalue by multisection on Sturm counts over 256 points (64 per
-//      wave, one barrier per round; theta_lb / hint as in block_check);
-//   2. the eigenvector from the two three-term recurrences of (T - theta) f = 0
-//      in the division-free minor form: with pi_k = beta_0 ... beta_{k-1},
-//      g_k = f_k pi_k obeys g_{k+1} = (theta - alpha_k) g_k - beta^2_{k-1} g_{k-1}
-//      (one fma on the chain) and Q_k = pi_k^2 runs beside it -- forward from
-//      the top on wave 0, backward (h, R) from the bottom on wave 1 at the same
-//      time, both rescaled by powers of two every four steps;
-//   3. every lane forms, for its two indices, the twisted-factorisation
-//      gamma_k = (alpha_k - theta) + beta^2_{k-1} g_{k-1}/g_k + beta^2_k h_{k+1}/h_k
-//      (= d+_k + d-_k - (alpha_k - theta)), the twist r = argmin |gamma| (first
-//      index), and z_k = (g_k/g_r) sqrt(Q_r/Q_k) (k <= r), (h_k/h_r) sqrt(R_r/R_k)
-//      (k >= r): the twisted factorisation's vector, each half from its stable
-//      direction; normalised.
-// scr: >= kCheckScr doubles of LDS.  Every wave returns the same values; wave
-// 0 writes z[0, m).  The residual of the pair is beta_m |z_{m-1}|.
-constexpr int kCheckScr = 6 * MMAX + 32;
-
-// Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a
-// workgroup-scope release fence, so it waits for the wave's outstanding
-// GLOBAL stores (vmcnt(0)) too -- in the Lanczos step that is the basis
-// vector just written to the per-workgroup scratch, an L2 round trip per
-// barrier for nothing the barrier protects.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-
-__device__ __forceinline__ void fast_check(const double* T, int m, double theta_lb, double hint, double glo,
-                                           double ghi, double* z, double* scr, double* theta_out, double* zlast_out,
-                                           int* rounds_out, long long* ph = nullptr) {
-  m = __builtin_amdgcn_readfirstlane(m);
-  if (ph) ph[0] = __builtin_amdgcn_s_memtime();
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* gq = scr;                   // [MMAX] g | [MMAX] Q  (forward chain)
-  double* hr = scr + 2 * MMAX;        // [MMAX] h | [MMAX] R  (backward chain)
-  double* ex = scr + 4 * MMAX;        // [MMAX] exponents (fwd g, Q per block of 4) | [MMAX] (bwd)
-  unsigned long long* masks = reinterpret_cast<unsigned long long*>(scr + 6 * MMAX);   // [2][4]
-  const double a0 = T[0];
-  double lo = fmax(glo, fmax(theta_lb, a0));
-  double hi = ghi;
-  if (!(lo < hi)) lo = glo;
-  const bool hinted = hint >= 0.0 && theta_lb > -1e299;
-  const double hg = lo + 4.0 * hint + 4e-16 * fabs(lo);
-  if (ph) ph[1] = __builtin_amdgcn_s_memtime();
-  // Sturm count at x (det(T_k - x) signs; >= m <=> x above every eigenvalue).
-  // fp64 fma latency (~30 cycles for one wave) sets the pace: one fma per
-  // step on the chain, the (alpha, beta^2) pairs read from LDS (broadcast) a
-  // block of four ahead of their use.
-  const double2* T2 = reinterpret_cast<const double2*>(T);
-  auto count = [&](double x) -> int {
-    double p2 = 1.0, p1 = a0 - x;
-    unsigned cnt = static_cast<unsigned>(__builtin_bit_cast(unsigned long long, p1) >> 63);
-    auto step = [&](double2 t) __attribute__((always_inline)) {
-      const double pk = fma(t.x - x, p1, -(t.y * p2));
-      cnt += static_cast<unsigned>((__builtin_bit_cast(unsigned long long, pk) ^
-                                    __builtin_bit_cast(unsigned long long, p1)) >> 63);
-      p2 = p1;
-      p1 = pk;
-    };
-    double2 c0 = T2[1], c1 = T2[2];
-    int q = 1;
-    for (; q + 4 <= m; q += 4) {
-      const double2 c2 = T2[q + 2], c3 = T2[q + 3];
-      step(c0);
-      step(c1);
-      c0 = T2[q + 4];
-      c1 = T2[q + 5];
-      step(c2);
-      step(c3);
-      const int e = __builtin_amdgcn_frexp_exp(p1);
-      p1 = __builtin_amdgcn_ldexp(p1, -e);
-      p2 = __builtin_amdgcn_ldexp(p2, -e);
-    }
-    if (q < m) step(c0);
-    if (q + 1 < m) step(c1);
-    if (q + 2 < m) step(T2[q + 2]);
-    return static_cast<int>(cnt);
-  };
-  // Cold start (no previous Ritz value in this eigenproblem): Laguerre's
-  // method from the Gershgorin upper bound on det(x - T_m) = P(x) -- from above
-  // the largest root of a real-rooted polynomial it decreases monotonically to
-  // it, cubically once close (4-6 chains of m steps instead of ~7 multisection
-  // rounds); one uniform round of 256 points over +-64 ulps then brackets it to
-  // two ulps and verifies that it is the top eigenvalue (else the full
-  // multisection runs from the Gershgorin bracket).  Every wave computes the
-  // same (wave-uniform) iterates.
-  bool laguerre = false;
-  const double lo0 = lo, hi0 = hi;
-  if (!hinted && m > 2) {
-    double x = hi;
-    for (int itl = 0; itl < 16; ++itl) {
-      double p0 = 1.0, p1 = x - a0, d0 = 0.0, d1 = 1.0, e0 = 0.0, e1 = 0.0;
-      auto lstep = [&](double2 t) __attribute__((always_inline)) {
-        const double c = x - t.x;
-        const double pn = fma(c, p1, -(t.y * p0));
-        const double dn = fma(c, d1, p1 - t.y * d0);
-        const double en = fma(c, e1, 2.0 * d1 - t.y * e0);
-        p0 = p1; p1 = pn;
-        d0 = d1; d1 = dn;
-        e0 = e1; e1 = en;
-      };
-      double2 c0 = T2[1], c1 = T2[2];
-      int q = 1;
-      for (; q + 4 <= m; q += 4) {
-        const double2 c2 = T2[q + 2], c3 = T2[q + 3];
-        lstep(c0);
-        lstep(c1);
-        c0 = T2[q + 4];
-        c1 = T2[q + 5];
-        lstep(c2);
-        lstep(c3);
-        const int e = __builtin_amdgcn_frexp_exp(fmax(fabs(p1), fabs(d1)));
-        p0 = __builtin_amdgcn_ldexp(p0, -e); p1 = __builtin_amdgcn_ldexp(p1, -e);
-        d0 = __builtin_amdgcn_ldexp(d0, -e); d1 = __builtin_amdgcn_ldexp(d1, -e);
-        e0 = __builtin_amdgcn_ldexp(e0, -e); e1 = __builtin_amdgcn_ldexp(e1, -e);
-      }
-      if (q < m) lstep(c0);
-      if (q + 1 < m) lstep(c1);
-      if (q + 2 < m) lstep(T2[q + 2]);
-      if (!(p1 != 0.0)) break;   // x is an eigenvalue (or a NaN appeared): the bracket round decides
-      const double G = d1 / p1, H = G * G - e1 / p1;
-      const double nn = static_cast<double>(m);
-      const double den = G + sqrt(fmax((nn - 1.0) * (nn * H - G * G), 0.0));
-      const double xn = x - nn / den;
-      if (!(xn < x) || !(xn >= lo0)) break;
-      const bool fin = x - xn <= 4e-16 * fabs(x);
-      x = xn;
-      if (fin) break;
-    }
-    const double u = 64.0 * 2.2204460492503131e-16 * fabs(x);
-    if (x - u > lo0 && x + u < hi0) {
-      lo = x - u;
-      hi = x + u;
-      laguerre = true;
-    }
-  }
-  int round = 0;
-  for (; round < 24; ++round) {
-    const int kind = round == 0 ? (laguerre ? 3 : (hinted && hg < hi ? 1 : 2)) : 0;
-    const double rlo = lo, rhi = hi;
-    // kind 3: the Laguerre bracket, points at both ends included so that the
-    // round also verifies it
-    auto point = [&](int p) -> double {
-      if (kind == 1) return p < 255 ? rlo + (hg - rlo) * ((p + 1) * (1.0 / 255.0)) : rhi;
-      if (kind == 2) return rlo + (rhi - rlo) * __builtin_amdgcn_ldexp(1.0, p - 255);
-      if (kind == 3) return rlo + (rhi - rlo) * (p * (1.0 / 255.0));
-      return rlo + (rhi - rlo) * ((p + 1) * (1.0 / 257.0));
-    };
-    const unsigned long long ok = __builtin_amdgcn_ballot_w64(count(point(64 * wave + lane)) >= m);
-    unsigned long long* M = masks + 4 * (round & 1);
-    if (lane == 0) M[wave] = ok;
-    lds_barrier();
-    int first = 256;
-    for (int w = 3; w >= 0; --w)
-      if (M[w]) first = 64 * w + __builtin_ctzll(M[w]);
-    if (kind == 3 && (first == 0 || first == 256)) {
-      // the top eigenvalue is not inside the Laguerre bracket: full multisection
-      lo = lo0;
-      hi = hi0;
-      laguerre = false;
-      continue;
-    }
-    const double xf = first < 256 ? point(first) : rhi;
-    const double xb = first > 0 ? point(first - 1) : rlo;
-    const bool stalled = xb == lo && xf == hi;
-    lo = xb;
-    hi = xf;
-    if (stalled || hi - lo <= 4.5e-16 * fmax(fabs(lo), fabs(hi))) break;
-  }
-  const double lm = 0.5 * (lo + hi);
-  if (ph) ph[2] = __builtin_amdgcn_s_memtime();
-  // ---- the two eigenvector recurrences: wave 0 forward (row i produces
-  // index i + 1), wave 1 backward (row i produces index i - 1)
-  auto chain = [&](auto FWD) __attribute__((always_inline)) {
-    constexpr bool fwd = decltype(FWD)::value;
-    double* val = fwd ? gq : hr;
-    double* exb = ex + (fwd ? 0 : MMAX);
-    double g1 = 1.0, g0 = 0.0, qq = 1.0;
-    int eg = 0, eq = 0, k = 0;   // k = steps done = position of g1 along the chain
-    const int i0 = fwd ? 0 : m - 1;
-    // lane l keeps the values of indices l and l + 64 in registers (written
-    // to LDS once, after the chain)
-    double gv[2] = {0.0, 0.0}, qv[2] = {0.0, 0.0};
-    if ((i0 & 63) == lane) {
-      gv[i0 >> 6] = 1.0;
-      qv[i0 >> 6] = 1.0;
-    }
-    if (lane == 0) {
-      exb[0] = 0.0;
-      exb[1] = 0.0;
-    }
-    // Pair P_i = T2[i] = (alpha_i, beta^2_{i-1}).  fwd row i = k: behind =
-    // P_i.y, ahead = beta^2_i = P_{i+1}.y (the next step's pair); bwd row
-    // i = m-1-k: ahead = P_i.y, behind = beta^2_i = P_{i+1}.y (the previous
-    // step's pair).  Pairs are read two steps ahead of use; reads past the
-    // chain's end land in the record's padding / row 0 and are never used.
-    auto pr = [&](int kk) __attribute__((always_inline)) -> double2 {
-      int i = fwd ? kk : m - 1 - kk;
-      i = i < 0 ? 0 : i;
-      return T2[i];
-    };
-    double2 cur = pr(0), nx1 = pr(1), nx2 = pr(2);
-    double bbw = 0.0;   // bwd: behind coefficient (previous pair's .y); fwd: unused
-    auto step = [&](double2 c, double2 nxt) __attribute__((always_inline)) {
-      const double behind = fwd ? c.y : bbw;
-      const double ahead = fwd ? nxt.y : c.y;
-      const double gn = fma(lm - c.x, g1, -(behind * g0));
-      qq *= ahead;
-      if (!fwd) bbw = c.y;
-      g0 = g1;
-      g1 = gn;
-      const int idx = fwd ? k + 1 : m - 2 - k;
-      if ((k & 3) == 3) {
-        const int e = __builtin_amdgcn_frexp_exp(g1);
-        g1 = __builtin_amdgcn_ldexp(g1, -e);
-        g0 = __builtin_amdgcn_ldexp(g0, -e);
-        eg += e;
-        const int e2 = __builtin_amdgcn_frexp_exp(qq);
-        qq = __builtin_amdgcn_ldexp(qq, -e2);
-        eq += e2;
-        if (lane == 0) {
-          exb[2 * ((k + 1) >> 2)] = static_cast<double>(eg);
-          exb[2 * ((k + 1) >> 2) + 1] = static_cast<double>(eq);
-        }
-      }
-      const bool me = (idx & 63) == lane;
-      if (idx < 64) {
-        gv[0] = me ? g1 : gv[0];
-        qv[0] = me ? qq : qv[0];
-      } else {
-        gv[1] = me ? g1 : gv[1];
-        qv[1] = me ? qq : qv[1];
-      }
-      ++k;
-    };
-    const int steps = m - 1;
-    while (k + 2 <= steps) {
-      const double2 nx3 = pr(k + 3), nx4 = pr(k + 4);
-      step(cur, nx1);
-      step(nx1, nx2);
-      cur = nx2;
-      nx1 = nx3;
-      nx2 = nx4;
-    }
-    if (k < steps) step(cur, nx1);
-    val[lane] = gv[0];
-    val[MMAX + lane] = qv[0];
-    val[64 + lane] = gv[1];
-    val[MMAX + 64 + lane] = qv[1];
-  };
-  // the first step's "behind" coefficient multiplies g0 = 0
-  const int wu = __builtin_amdgcn_readfirstlane(wave);
-  if (wu == 0) chain(std::integral_constant<bool, true>{});
-  else if (wu == 1) chain(std::integral_constant<bool, false>{});
-  lds_barrier();
-  if (ph) ph[3] = __builtin_amdgcn_s_memtime();
-  // exponents of a chain value by its position p along the chain: the rescale
-  // after step 4b+3 makes position 4b+4 the first of block b+1
-  auto pexp = [&](const double* exb, int p, int which) -> int {
-    return static_cast<int>(exb[2 * (p >> 2) + which]);
-  };
-  // ---- gamma, twist, z (every wave, identical)
-  double zv[2], gam = 1e308;
-  int tw = 0;
-#pragma unroll 1
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const int k = lane + 64 * s2;
-    zv[s2] = 0.0;
-    if (k < m) {
-      double g = T[2 * k] - lm;
-      if (k > 0)
-        g += T[2 * k + 1] * __builtin_amdgcn_ldexp(gq[k - 1] * rcp_nr(gq[k]), pexp(ex, k - 1, 0) - pexp(ex, k, 0));
-      if (k + 1 < m)
-        g += T[2 * k + 3] * __builtin_amdgcn_ldexp(hr[k + 1] * rcp_nr(hr[k]),
-                                             pexp(ex + MMAX, m - 2 - k, 0) - pexp(ex + MMAX, m - 1 - k, 0));
-      const double ga = fabs(g);
-      if (ga < gam) {
-        gam = ga;
-        tw = k;
-      }
-    }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double og = __shfl_xor(gam, off);
-    const int ot = __shfl_xor(tw, off);
-    if (og < gam || (og == gam && ot < tw)) {
-      gam = og;
-      tw = ot;
-    }
-  }
-  tw = __builtin_amdgcn_readfirstlane(tw);
-  if (ph) ph[4] = __builtin_amdgcn_s_memtime();
-  const double igr = rcp_nr(gq[tw]), ihr = rcp_nr(hr[tw]);
-  const double qr = gq[MMAX + tw], rr = hr[MMAX + tw];
-  const int egr = pexp(ex, tw, 0), eqr = pexp(ex, tw, 1);
-  const int ehr = pexp(ex + MMAX, m - 1 - tw, 0), err = pexp(ex + MMAX, m - 1 - tw, 1);
-#pragma unroll 1
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const int k = lane + 64 * s2;
-    if (k < m) {
-      if (k <= tw) {   // (g_k / g_r) sqrt(Q_r / Q_k)
-        int e2 = eqr - pexp(ex, k, 1);
-        double qratio = qr * rcp_nr(gq[MMAX + k]);
-        if (e2 & 1) { qratio *= 2.0; e2 -= 1; }
-        zv[s2] = __builtin_amdgcn_ldexp(gq[k] * igr * sqrt(qratio), pexp(ex, k, 0) - egr + e2 / 2);
-      } else {         // (h_k / h_r) sqrt(R_r / R_k)
-        int e2 = err - pexp(ex + MMAX, m - 1 - k, 1);
-        double rratio = rr * rcp_nr(hr[MMAX + k]);
-        if (e2 & 1) { rratio *= 2.0; e2 -= 1; }
-        zv[s2] = __builtin_amdgcn_ldexp(hr[k] * ihr * sqrt(rratio), pexp(ex + MMAX, m - 1 - k, 0) - ehr + e2 / 2);
-      }
-    }
-  }
-  const double inv = 1.0 / sqrt(wave_sum(zv[0] * zv[0] + zv[1] * zv[1]));
-  if (wave == 0) {
-    if (lane < m) z[lane] = zv[0] * inv;
-    if (lane + 64 < m) z[lane + 64] = zv[1] * inv;
-  }
-  lds_barrier();   // z is read by every wave (the Ritz vector) after the caller's next step or none
-  *zlast_out = rl_any(zv, m - 1) * inv;
-  *theta_out = lm;
-  *rounds_out = round + 1;
-  if (ph) ph[5] = __builtin_amdgcn_s_memtime();
-}
-
-// ---- lanczos_solve_kernel (round 3 layout) -------------------------------
-// Wave w holds rows 32w .. 32w + 31 of M: lane l has row 32w + (l & 31), the
-// column half 64 * (l >> 5) .. + 63 (64 doubles).  A 16-lane DPP row therefore
-// shares one column half, so the operator input reaches every lane through
-// v_fmac_f64_dpp row_newbcast (lane k of the DPP row holds x[64 half + 4k ..
-// + 3], two ds_read_b128 per lane per step instead of 32), and the two halves
-// of a row are added with one v_permlane32_swap (tools/ubench/lanczos_step.hip:
-// 1.68k vs 2.28k cycles per step alone, 1.23 vs 1.67 us per step at 3
-// workgroups per CU).
-constexpr int kTrw = 2 * MMAX + 32;   // T record: (alpha_q, beta^2_{q-1}) pairs, padded for the check's prefetch
-
-constexpr size_t kLanczosLds =
-    sizeof(double) * (136 + 2 * 136 + 32 + kTrw + 2 * MMAX + kCheckScr + 64 + 4 * FNP + 240) +
-    sizeof(int) * (3 * FNP + 16);
-static_assert(3 * kLanczosLds <= 163840, "three solver workgroups must fit one CU's LDS");
-// The first kLdsBasis Lanczos vectors stay in LDS (the registers cap the solver
-// at two workgroups per CU, which leaves ~58 KiB of LDS each); only steps past
-// them go to the per-workgroup global scratch.  Round 3's whole-op PMC had the
-// scratch basis at 109 GB read + 33 GB written per C4 call: 512 workgroups x
-// ~70 vectors of 1 KiB do not stay in the L2.
-constexpr int kLdsBasis = 56;
-constexpr size_t kLanczosLdsTotal = kLanczosLds + sizeof(double) * kLdsBasis * FNP;
-static_assert(2 * kLanczosLdsTotal <= 163840, "two solver workgroups with their LDS basis must fit one CU");
-
-__device__ __forceinline__ double swap_halves(double v) {   // the value of lane l ^ 32
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(b), static_cast<unsigned>(b), false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(b >> 32), static_cast<unsigned>(b >> 32),
-                                                   false, false);
-  const bool up = (threadIdx.x & 63) >= 32;
-  const unsigned l = up ? lo[0] : lo[1], h = up ? hi[0] : hi[1];
-  return __builtin_bit_cast(double, (static_cast<unsigned long long>(h) << 32) | l);
-}
-
-#define SRA_FMAC_DPP(K, J)                                                                       \
-  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #K " row_mask:0xf bank_mask:0xf"        \
-               : "+v"(acc[J])                                                                     \
-               : "v"(xr[J]), "v"(g[4 * K + J]))
-#define SRA_FMAC_DPP4(K) SRA_FMAC_DPP(K, 0); SRA_FMAC_DPP(K, 1); SRA_FMAC_DPP(K, 2); SRA_FMAC_DPP(K, 3)
-
-template <int MODE, bool DBG>
-__global__ void __launch_bounds__(256, 2) lanczos_solve_kernel(SolveArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* xbuf = reinterpret_cast<double*>(smem);   // [136] operator input
-  double* gbuf = xbuf + 136;                        // [136] g = G w (forming M)
-  double* sbuf = gbuf + 136;                        // [136] sqrt(w)
-  double* red = sbuf + 136;                         // [2][16] block reductions (parity slots)
-  double* trw = red + 32;                           // [kTrw] tridiagonal record
-  double* zbuf = trw + kTrw;                        // [2][MMAX] eigenvectors of T (current / best check)
-  double* cscr = zbuf + 2 * MMAX;                   // [kCheckScr] check scratch
-  double* hbuf = cscr + kCheckScr;                  // [64] projection scalar
-  double* cvec = hbuf + 64;                         // [FNP] weights (projection / final scale)
-  double* vscr = cvec + FNP;                        // [3][FNP] projection scratch
-  double* clog = vscr + 3 * FNP;                    // [60][4] DBG: check log of the current iteration
-  int* ibuf = reinterpret_cast<int*>(clog + 240);   // [3][FNP] int scratch + [16] argmax slots
-  double* lbas = reinterpret_cast<double*>(smem + kLanczosLds);   // [kLdsBasis][FNP] first basis vectors
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int row = 32 * wave + (lane & 31);
-  const int half = lane >> 5;
-  const bool own = half == 0;
-  const int n = A.n;
-  double* Vb = A.Vg + static_cast<size_t>(blockIdx.x) * MMAX * FNP;
-  // basis entry qq of this row: LDS for the first kLdsBasis vectors, else the scratch
-  auto vload = [&](int qq) __attribute__((always_inline)) -> double {
-    return qq < kLdsBasis ? lbas[qq * FNP + row] : Vb[qq * FNP + row];
-  };
-
-  int rslot = 0;
-  auto reduce2 = [&](double v0, double v1, double (&o)[4], int nv) __attribute__((always_inline)) {
-    v0 = wave_sum(v0);
-    if (nv > 1) v1 = wave_sum(v1);
-    double* R = red + 16 * rslot;
-    if (lane == 0) {
-      R[4 * wave + 0] = v0;
-      if (nv > 1) R[4 * wave + 1] = v1;
-    }
-    lds_barrier();
-    o[0] = (R[0] + R[4]) + (R[8] + R[12]);
-    if (nv > 1) o[1] = (R[1] + R[5]) + (R[9] + R[13]);
-    rslot ^= 1;
-  };
-  auto argmax_first = [&](double v, int i, double* vbest) __attribute__((always_inline)) -> int {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const double ov = __shfl_xor(v, off);
-      const int oi = __shfl_xor(i, off);
-      if (ov > v || (ov == v && oi < i)) {
-        v = ov;
-        i = oi;
-      }
-    }
-    double* R = red + 16 * rslot;
-    int* I = ibuf + 3 * FNP + 8 * rslot;
-    if (lane == 0) {
-      R[wave] = v;
-      I[wave] = i;
-    }
-    lds_barrier();
-    double bv = R[0];
-    int bi = I[0];
-    for (int q = 1; q < 4; ++q)
-      if (R[q] > bv || (R[q] == bv && I[q] < bi)) {
-        bv = R[q];
-        bi = I[q];
-      }
-    rslot ^= 1;
-    *vbest = bv;
-    return bi;
-  };
-  if (tid < 16) trw[2 * MMAX + tid] = 0.0;   // prefetch padding of the T record
-  int* qslot = ibuf + 3 * FNP + 16 - 1;       // the chunk this workgroup took from the queue
-
-  // chunks come from a work queue (A.fb_count[4]): their cost varies with the
-  // Lanczos steps they need, a static split leaves a tail
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) *qslot = atomicAdd(A.fb_count + 4, 1);
-    __syncthreads();
-    const int ch = *qslot;
-    if (ch >= A.nb) break;
-    const double2* Gr = reinterpret_cast<const double2*>(A.G + static_cast<size_t>(ch) * FNP * FNP + row * FNP +
-                                                         64 * half);
-    double g[64];   // G's row segment at the start of an iteration, then M's
-    // y = (this register matrix) x for x in xbuf; both lanes of the row get the value
-    auto gmv = [&]() __attribute__((always_inline)) -> double {
-      const double2* xp = reinterpret_cast<const double2*>(xbuf + 64 * half + 4 * (lane & 15));
-      const double2 xa = xp[0], xb = xp[1];
-      double xr[4] = {xa.x, xa.y, xb.x, xb.y};
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      SRA_FMAC_DPP4(0); SRA_FMAC_DPP4(1); SRA_FMAC_DPP4(2); SRA_FMAC_DPP4(3);
-      SRA_FMAC_DPP4(4); SRA_FMAC_DPP4(5); SRA_FMAC_DPP4(6); SRA_FMAC_DPP4(7);
-      SRA_FMAC_DPP4(8); SRA_FMAC_DPP4(9); SRA_FMAC_DPP4(10); SRA_FMAC_DPP4(11);
-      SRA_FMAC_DPP4(12); SRA_FMAC_DPP4(13); SRA_FMAC_DPP4(14); SRA_FMAC_DPP4(15);
-      const double p = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      return p + swap_halves(p);
-    };
-
-    const bool dbg = DBG && ch == 0;
-    bool ai;
-    if constexpr (MODE == 1) ai = A.act[static_cast<size_t>(ch) * FNP + row] != 0;
-    else ai = row < n;
-    double ci = ai ? 1.0 : 0.0;
-    const int fdrop = static_cast<int>(ceil(A.eps * n));
-    const int n_keep = MODE == 1 ? n - (fdrop < n ? fdrop : n) : n;
-    const double step = MODE == 1 ? A.misc[static_cast<size_t>(ch) * kMisc + 1] : 0.0;
-    const int iters = MODE == 0 ? 2 * static_cast<int>(A.eps * n) : static_cast<int>(2 * A.eps * n_keep);
-    int m_hint = 24;
-    double rate_hint = 0.0;
-    bool fallback = false;
-    int clog_n = 0;
-    int done = 0;
-    int* tr = A.trace != nullptr ? A.trace + static_cast<size_t>(ch) * kTraceStride : nullptr;
-    // ex_noregret damps the top direction gently, so the previous iteration's
-    // Ritz vector is a near-eigenvector of the next M: warm start from it
-    // (filterL2's next top vector is essentially new)
-    double u_prev = 0.0;
-    bool have_u = false;
-
-    // G into registers (at the end of every iteration for the next one, as
-    // soon as M's last matvec has read them: the loads overlap the decision's
-    // reductions)
-    auto load_g = [&]() __attribute__((always_inline)) {
-#pragma unroll
-      for (int c = 0; c < 32; ++c) {
-        const double2 v = Gr[c];
-        g[2 * c] = v.x;
-        g[2 * c + 1] = v.y;
-      }
-    };
-    load_g();
-    for (int it = 0; it < iters; ++it) {
-      const long long t_it = dbg ? clock64() : 0;
-      if (DBG) clog_n = 0;
-      // ---- weights, g = G w, s = w^T G w (G in registers)
-      double o[4];
-      reduce2(own && ai ? ci : 0.0, own && ai ? 1.0 : 0.0, o, 2);
-      const double csum = o[0];
-      const int nact = static_cast<int>(o[1]);
-      const double wi = ai ? ci / csum : 0.0;
-      const double swi = sqrt(wi > 0.0 ? wi : 0.0);
-      if (own) {
-        xbuf[row] = wi;
-        sbuf[row] = swi;
-      }
-      lds_barrier();
-      const double gwi = gmv();
-      if (own) gbuf[row] = gwi;
-      reduce2(own ? wi * gwi : 0.0, 0.0, o, 1);
-      const double sgw = o[0];
-      // ---- M = W^1/2 (G - g 1^T - 1 g^T + s 1 1^T) W^1/2 in place
-      {
-        const double2* gh = reinterpret_cast<const double2*>(gbuf + 64 * half);
-        const double2* sh = reinterpret_cast<const double2*>(sbuf + 64 * half);
-        const double ri = sgw - gwi;
-#pragma unroll
-        for (int c = 0; c < 32; ++c) {
-          const double2 gj = gh[c], sj = sh[c];
-          g[2 * c] = swi * ((g[2 * c] + ri - gj.x) * sj.x);
-          g[2 * c + 1] = swi * ((g[2 * c + 1] + ri - gj.y) * sj.y);
-          // at most four (g, sqrt w) pieces in flight: the compiler would
-          // otherwise hoist all 64 LDS reads (128 VGPRs beside the 128 of M)
-          if ((c & 3) == 3) asm volatile("" : "+v"(g[2 * c]), "+v"(g[2 * c + 1])::"memory");
-        }
-      }
-
-      // ---- top eigenpair of M by plain Lanczos (see the round-2 notes above
-      // lanczos_solve_kernel's declaration history in DESIGN.md k6): checks by
-      // fast_check, best residual kept, a ghost retries once with dense checks
-      double lam = 0.0, resid = 0.0, ui = 0.0;
-      int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
-      bool converged = false;
-      double tscale = 0.0;
-      long long tcheck = 0;
-      int trounds = 0;
-      // attempt 0: plain Lanczos; 1: after a ghost, again with dense checks;
-      // 2: with full re-orthogonalisation against the stored basis (the rare
-      // chunk whose top pair plain Lanczos cannot resolve is finished here, in
-      // its own iteration, instead of being redone on the fallback kernel)
-      for (int attempt = 0; attempt < 3 && !converged; ++attempt) {
-        const bool reorth = attempt == 2;
-        // ex_noregret's weights integrate every iteration's eigenvector (no
-        // removal resets them): the re-orthogonalising solver's bound there
-        const double acc_tol = MODE == 1 ? kResTol : kAccept;
-        double rt;
-        const bool warm = MODE == 1 && A.warm && have_u && attempt == 0;
-        {
-          const double hh = 0.5 + (row * 0.6180339887498949 - floor(row * 0.6180339887498949));
-          rt = swi > 0.0 ? (warm ? u_prev + 1e-3 * swi * hh : swi * hh) : 0.0;
-        }
-        if (own) xbuf[row] = rt;
-        reduce2(own ? rt * rt : 0.0, 0.0, o, 1);
-        double nrm2 = o[0];
-        double qprev = 0.0, theta_lb = -1e300, hint = -1.0;
-        double res_best = 1e300, lam_best = 0.0;
-        tscale = 0.0;
-        // incremental Gershgorin bounds of T: rows 0 .. j-2 final, plus row j-1
-        double gfin_hi = -1e300, gfin_lo = 1e300, a_last = 0.0, b_prev = 0.0;
-        const int adv_max = attempt == 1 ? 1 : A.max_adv;
-        const int first = warm ? 1 : (m_hint + A.first_off > 4 ? m_hint + A.first_off : 4);
-        int next_check = attempt == 1 ? (m_retry > 4 ? m_retry : 4) : first;
-        int m_a = -1, m_last = 4, m_pre = 4;
-        double res_a = 0.0;
-        bool ghost = false;
-        for (int j = 0;; ++j) {
-          const double bet = sqrt(nrm2);
-          if (j > 0) {
-            if (tid == 0) trw[2 * j + 1] = nrm2;
-            tscale = fmax(tscale, bet);
-            const bool breakdown = !(bet > 1e-14 * tscale);
-            if (breakdown || j == MMAX || j >= next_check) {
-              const int m = j;
-              ++nchecks;
-              const long long tc0 = dbg ? clock64() : 0;
-              double lm, zl;
-              int rounds = 0;
-              const double ghi = fmax(gfin_hi, a_last + b_prev), glo = fmin(gfin_lo, a_last - b_prev);
-              fast_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, cscr, &lm, &zl, &rounds);
-              if (dbg) {
-                tcheck += clock64() - tc0;
-                trounds += rounds;
-              }
-              const double res = fabs(bet * zl);
-              if (DBG && tid == 0 && clog_n < 60) {
-                double* lg = clog + 4 * clog_n;
-                lg[0] = m + 1000.0 * attempt + 10000.0 * it;
-                lg[1] = lm;
-                lg[2] = zl;
-                lg[3] = bet;
-              }
-              ++clog_n;
-              hint = theta_lb > -1e299 ? fmax(lm - theta_lb, 0.0) : -1.0;
-              theta_lb = lm;
-              if (res <= acc_tol * fabs(lm) || breakdown) {
-                converged = true;
-                m_conv = m;
-                lam = lm;
-                resid = res;
-                zbest = zcur;
-                break;
-              }
-              const bool better = res < res_best;
-              if (better) {
-                m_pre = m_last;
-                res_best = res;
-                lam_best = lm;
-                zbest = zcur;
-                zcur ^= 1;
-              }
-              ghost = !reorth && res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
-              const bool out_of_steps = j == MMAX;
-              if (ghost || out_of_steps) {
-                if (tid == 0) atomicAdd(A.fb_count + (ghost ? (attempt == 0 ? 3 : 1) : 2), 1);
-                if (!ghost && attempt < 2) {   // out of steps: straight on to the re-orthogonalising attempt
-                  ghost = true;
-                  attempt = 1;
-                }
-                m_retry = m_pre;
-                break;
-              }
-              int adv = 4;
-              double rate = rate_hint;
-              if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
-              if (rate < 0.0 && res > 0.0) {
-                const double need = log(acc_tol * fabs(lm) / res) / rate;
-                adv = need < 1.0 ? 1 : (need > adv_max ? adv_max : static_cast<int>(ceil(need)));
-              }
-              m_a = m;
-              res_a = res;
-              m_last = m;
-              next_check = m + adv;
-            }
-            // row j-1 is final now that beta_{j-1} is known
-            gfin_hi = fmax(gfin_hi, a_last + b_prev + bet);
-            gfin_lo = fmin(gfin_lo, a_last - b_prev - bet);
-            b_prev = bet;
-          }
-          // y = M r~ (r~ = beta q_j in xbuf), alpha_j = q_j . M q_j
-          const double y = gmv();
-          const double ib = 1.0 / bet;
-          const double q = rt * ib;
-          if (own) {
-            if (j < kLdsBasis) lbas[j * FNP + row] = q;
-            else Vb[j * FNP + row] = q;
-          }
-          const double mq = y * ib;
-          reduce2(own ? q * mq : 0.0, 0.0, o, 1);
-          double aj = o[0];
-          double r = mq - aj * q - (j > 0 ? bet * qprev : 0.0);
-          if (reorth) {
-            // classical Gram-Schmidt against q_0 .. q_j (the own lanes' basis
-            // entries, read back by both lanes of the row after the stores
-            // landed), a second pass when |r|^2 drops below half (DGKS); alpha
-            // takes the q_j coefficients
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            constexpr int HS = MMAX + 2;
-            double* hs = cscr;            // [4][HS] per-wave sums
-            double* hb = cscr + 4 * HS;   // [HS] block sums
-            for (int pass = 0; pass < 2; ++pass) {
-              const int nh = pass == 0 ? j + 2 : j + 1;
-              for (int qq = 0; qq < nh; ++qq) {
-                double v = own ? (qq <= j ? vload(qq) * r : r * r) : 0.0;
-                v = wave_sum(v);
-                if (lane == 0) hs[wave * HS + qq] = v;
-              }
-              lds_barrier();
-              if (tid < nh) hb[tid] = (hs[tid] + hs[HS + tid]) + (hs[2 * HS + tid] + hs[3 * HS + tid]);
-              lds_barrier();
-              double upd = 0.0, hn2 = 0.0;
-              for (int qq = 0; qq <= j; ++qq) {
-                const double hv = hb[qq];
-                upd = fma(hv, vload(qq), upd);
-                hn2 = fma(hv, hv, hn2);
-              }
-              r -= upd;
-              aj += hb[j];
-              const bool again = pass == 0 && hb[j + 1] - hn2 < kDgks * hb[j + 1];
-              lds_barrier();   // hb / hs are rewritten by the next pass or check
-              if (!again) break;
-            }
-          }
-          if (tid == 0) trw[2 * j] = aj;
-          a_last = aj;
-          tscale = fmax(tscale, fabs(aj));
-          qprev = q;
-          rt = r;
-          if (own) xbuf[row] = r;
-          reduce2(own ? r * r : 0.0, 0.0, o, 1);
-          nrm2 = o[0];
-        }
-        if (!ghost) break;
-      }
-      if (!converged) {
-        fallback = true;
-        break;
-      }
-      // ---- Ritz vector u = V z of the accepted check (the basis rows this
-      // wave's even lanes stored; let the stores land before reading them back)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      {
-        const double* zb = zbuf + zbest * MMAX;
-        double u0 = 0.0, u1 = 0.0;
-        int qq = 0;
-        for (; qq + 1 < m_conv; qq += 2) {
-          u0 = fma(zb[qq], vload(qq), u0);
-          u1 = fma(zb[qq + 1], vload(qq + 1), u1);
-        }
-        if (qq < m_conv) u0 = fma(zb[qq], vload(qq), u0);
-        ui = swi > 0.0 ? u0 + u1 : 0.0;
-      }
-      u_prev = ui;
-      have_u = true;
-      m_hint = m_conv > 8 ? m_conv : 8;
-      if (dbg && it < 256) {
-        double* rec = A.dbg + FNP * FNP + static_cast<int64_t>(it) * kDbgRec;
-        if (own) rec[row] = ci;
-        if (tid == 0) {
-          rec[FNP] = lam;
-          rec[FNP + 1] = m_conv;
-          rec[FNP + 2] = resid;
-          rec[FNP + 3] = nchecks;
-          rec[FNP + 4] = nact;
-          rec[FNP + 5] = sgw;
-          rec[FNP + 6] = 0;
-          rec[FNP + 7] = 0;
-          rec[FNP + 8] = static_cast<double>(clock64() - t_it);
-          rec[FNP + 9] = static_cast<double>(tcheck);
-          rec[FNP + 10] = 0;
-          rec[FNP + 11] = 0;
-          rec[FNP + 12] = trounds;
-        }
-      }
-      // ---- early exit (robust_estimator.py:163-164 / :71-72)
-      if (lam * lam <= A.expansion * A.sigma * A.sigma) break;
-      // ---- tau_i = ((M u)_i / sqrt(w_i))^2 / lambda
-      if (own) xbuf[row] = ui;
-      lds_barrier();
-      const double mu_i = gmv();
-      if (it + 1 < iters) load_g();   // M is dead: G back for the next iteration
-      const double cu = swi > 0.0 ? mu_i / swi : 0.0;
-      const double ti = cu * cu / lam;
-      if constexpr (MODE == 0) {
-        double tmax = 0.0;
-        const int p = argmax_first(own && ai ? ti : -__builtin_inf(), row, &tmax);
-        const double cn = (ai && row != p) ? ci * (1.0 - ti / tmax) : 0.0;
-        reduce2(own ? fabs(cn) : 0.0, 0.0, o, 1);
-        ci = cn / o[0];
-        if (row == p) ai = false;
-        if (tr != nullptr && tid == 0) tr[1 + it] = p;
-      } else {
-        const int nk = n_keep;
-        const double cap = 1.0 / (1.0 - A.eps) / nk;
-        if (ai) ci = ci * (1.0 - step * ti);
-        int capped = 0;
-        if (!kl_project(&ci, ai, row, own, nk, cap, cvec, vscr, ibuf, red, hbuf, &capped)) {
-          if (tid == 0) *A.status = 2;
-          break;
-        }
-        if (tr != nullptr && tid == 0) tr[1 + it] = capped;
-      }
-      done = it + 1;
-      lds_barrier();   // every wave's gmv reads of xbuf before the next iteration writes it
-    }
-
-    lds_barrier();
-    if (fallback) {
-      if (tid == 0) {
-        const int k = atomicAdd(A.fb_count, 1);
-        A.fb_list[k] = ch;
-        if (DBG && k == 0 && A.dbg != nullptr) {
-          double* lg = A.dbg + FNP * FNP + 250 * kDbgRec;
-          for (int e = 0; e < 4 * (clog_n < 60 ? clog_n : 60); ++e) lg[e] = clog[e];
-        }
-      }
-      continue;
-    }
-    if (own) {
-      cvec[row] = ai ? ci : 0.0;
-      ibuf[2 * FNP + row] = ai ? 1 : 0;
-      A.c[static_cast<size_t>(ch) * FNP + row] = ai ? ci : 0.0;
-      A.act[static_cast<size_t>(ch) * FNP + row] = ai ? 1 : 0;
-      if (tr != nullptr) tr[1 + FNP + row] = ai ? 1 : 0;
-    }
-    if (tr != nullptr && tid == 0) tr[0] = done;
-    lds_barrier();
-    if (tid == 0) {
-      int q2 = 0;
-      double* kept = vscr;
-      for (int i = 0; i < n; ++i)
-        if (ibuf[2 * FNP + i]) kept[q2++] = cvec[i];
-      A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
-    }
-    lds_barrier();
-  }
-}
-
-__global__ void list_all_kernel(int* list, int* count, int nb) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < nb) list[i] = i;
-  if (i == 0) *count = nb;
-}
+// (round 5: the four-wave lanczos_solve_kernel with its block_check /
+// fast_check checks was replaced by wave_solve_kernel, filter_wave.hip;
+// DESIGN.md k6 keeps its measurements)
 
 // ============================================================================
 // chunk_mean_kernel: the weighted mean of every coordinate of the batch
@@ -2767,9 +1728,6 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
                                 : (dbg ? reinterpret_cast<const void*>(&filter_solve_kernel<1, true>)
                                        : reinterpret_cast<const void*>(&filter_solve_kernel<1, false>));
   SRA_HIP(hipFuncSetAttribute(solve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kSolveLds)));
-  const void* lsolve = dbg ? reinterpret_cast<const void*>(&lanczos_solve_kernel<0, true>)
-                           : reinterpret_cast<const void*>(&lanczos_solve_kernel<0, false>);
-  SRA_HIP(hipFuncSetAttribute(lsolve, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLanczosLdsTotal)));
   for (int64_t c0 = 0; c0 < nchunks; c0 += bmax) {
     const int nb = static_cast<int>(nchunks - c0 < bmax ? nchunks - c0 : bmax);
     GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws, bs, nsrc, Bws, ldb};

@@ -52,7 +52,9 @@ constexpr int kExStride = 72;                 // check: exponents per block of 4
 constexpr int kWScr = 4 * MMAX + 2 * kExStride;   // operand (256) + group shifts (384) | check scratch
 static_assert(kWScr >= wsym::kZd + wsym::kTb, "the check scratch overlays the matvec scratch");
 constexpr int kWTrw = 2 * MMAX + 32;          // T record: (alpha_q, beta^2_{q-1}) pairs + prefetch padding
-constexpr size_t kWaveLds = sizeof(double) * (static_cast<size_t>(WKL) * FNP + kWScr + kWTrw + 2 * MMAX);
+// LDS per wave: C's LDS diagonals, the matvec / check scratch, the T record,
+// its reversed copy (the backward chain), the accepted check's eigenvector
+constexpr size_t kWaveLds = sizeof(double) * (static_cast<size_t>(WKL) * FNP + kWScr + 2 * kWTrw + MMAX);
 static_assert(4 * kWaveLds <= 163840, "four one-wave solvers must fit one CU's LDS");
 constexpr int kWaveGrid = 1024;               // 4 waves per CU x 256 CUs; each owns a basis slot
 constexpr double kEps = 1.1102230246251565e-16;       // unit roundoff
@@ -88,7 +90,7 @@ __device__ __forceinline__ void tstream(const double2* T2, int m, F&& f, G&& g) 
 // Returns theta (2-ulp bracket midpoint), the last component of the
 // normalised eigenvector (the residual is beta_m |z_{m-1}|), and writes z[0, m).
 __device__ __forceinline__ void wave_check(const double* T, int m, double theta_lb, double hint, double glo,
-                                           double ghi, double* z, double* scr, double* theta_out,
+                                           double ghi, double* z, double* scr, double* trev, double* theta_out,
                                            double* zlast_out, int* rounds_out, long long* ph = nullptr) {
   m = __builtin_amdgcn_readfirstlane(m);
   long long tp = ph ? clock64() : 0;
@@ -221,112 +223,90 @@ __device__ __forceinline__ void wave_check(const double* T, int m, double theta_
   stamp(1);
   // ---- the two eigenvector recurrences of (T - lm) f = 0 in the division-
   // free minor form (fast_check), forward from the top and backward from the
-  // bottom, interleaved; rescaled by powers of two every four steps
+  // bottom, rescaled by powers of two every four steps.  Round 5: lanes 0-31
+  // run the forward chain on T, lanes 32-63 the same code on the reversed
+  // record T'2[q] = (alpha_{m-1-q}, beta^2_{m-q}) -- the backward recurrence
+  // is the forward one of J T J -- so one instruction stream carries both
+  // chains (half the issue slots of running both in every lane)
   {
-    double* exf = ex;
-    double* exb = ex + kExStride;
-    double fg1 = 1.0, fg0 = 0.0, fq = 1.0, bg1 = 1.0, bg0 = 0.0, bq = 1.0, bbw = 0.0;
-    int feg = 0, feq = 0, beg = 0, beq = 0;
-    // chain values are wave-uniform: lane 0 stores each (g, Q) pair straight
-    // into the scratch (no per-lane select of the index's owner)
-    if (lane == 0) {
-      exf[0] = exf[1] = exb[0] = exb[1] = 0.0;
-      gq[0] = 1.0;
-      gq[MMAX] = 1.0;
-      hr[m - 1] = 1.0;
-      hr[MMAX + m - 1] = 1.0;
+    const bool fwd = lane < 32;
+    double2* Tr2 = reinterpret_cast<double2*>(trev);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int q = lane + 64 * s2;
+      if (q < m) Tr2[q] = double2{T[2 * (m - 1 - q)], q > 0 ? T[2 * (m - q) + 1] : 0.0};
+      else if (q < m + 8) Tr2[q] = double2{0.0, 0.0};   // the prefetch padding
     }
-    // chain values are wave-uniform: lane 0 stores them, a block of four steps
-    // at a time (one exec-mask region per block, so the steps' fp64 chains are
-    // scheduled without a branch between them)
-    auto put = [&](double* v, int idx, double g, double q) __attribute__((always_inline)) {
-      if (lane == 0) {
-        v[idx] = g;
-        v[MMAX + idx] = q;
-      }
-    };
-    // forward step k: pair k (carried) and pair k + 1; backward step k: pair
-    // m - 1 - k; both streams read a block of four ahead (tstream)
-    double2 fc = T2[0];
-    auto step = [&](double2 fn, double2 bc) __attribute__((always_inline)) {
-      const double fgn = fma(lm - fc.x, fg1, -(fc.y * fg0));
-      fq *= fn.y;
-      fg0 = fg1;
-      fg1 = fgn;
-      fc = fn;
-      const double bgn = fma(lm - bc.x, bg1, -(bbw * bg0));
-      bq *= bc.y;
-      bbw = bc.y;
-      bg0 = bg1;
-      bg1 = bgn;
+    wsym::lds_order();
+    const double2* S2 = fwd ? T2 : Tr2;
+    double* v = fwd ? gq : hr;                        // [MMAX] g | [MMAX] Q, or h | R
+    double* exs = fwd ? ex : ex + kExStride;
+    // the value of step k lands at k + 1 (forward) / m - 2 - k (backward)
+    const int i0 = fwd ? 1 : m - 2, di = fwd ? 1 : -1;
+    const bool wr = lane == 0 || lane == 32;          // one writer per chain
+    double g1 = 1.0, g0 = 0.0, qv = 1.0;
+    int eg = 0, eq = 0;
+    if (wr) {
+      exs[0] = exs[1] = 0.0;
+      v[fwd ? 0 : m - 1] = 1.0;
+      v[MMAX + (fwd ? 0 : m - 1)] = 1.0;
+    }
+    double2 c = S2[0];
+    auto step = [&](double2 nx) __attribute__((always_inline)) {
+      const double gn = fma(lm - c.x, g1, -(c.y * g0));
+      qv *= nx.y;
+      g0 = g1;
+      g1 = gn;
+      c = nx;
     };
     auto rescale_values = [&]() __attribute__((always_inline)) {
-      int e = __builtin_amdgcn_frexp_exp(fg1);
-      fg1 = __builtin_amdgcn_ldexp(fg1, -e);
-      fg0 = __builtin_amdgcn_ldexp(fg0, -e);
-      feg += e;
-      e = __builtin_amdgcn_frexp_exp(fq);
-      fq = __builtin_amdgcn_ldexp(fq, -e);
-      feq += e;
-      e = __builtin_amdgcn_frexp_exp(bg1);
-      bg1 = __builtin_amdgcn_ldexp(bg1, -e);
-      bg0 = __builtin_amdgcn_ldexp(bg0, -e);
-      beg += e;
-      e = __builtin_amdgcn_frexp_exp(bq);
-      bq = __builtin_amdgcn_ldexp(bq, -e);
-      beq += e;
+      int e = __builtin_amdgcn_frexp_exp(g1);
+      g1 = __builtin_amdgcn_ldexp(g1, -e);
+      g0 = __builtin_amdgcn_ldexp(g0, -e);
+      eg += e;
+      e = __builtin_amdgcn_frexp_exp(qv);
+      qv = __builtin_amdgcn_ldexp(qv, -e);
+      eq += e;
     };
     const int steps = m - 1;
-    // pair indices m-1-k for the backward stream are >= 0 for k < m; the reads
-    // past the chain's end (k >= steps) land on valid record slots and are unused
-    auto bidx = [&](int k) { return m - 1 - k < 0 ? 0 : m - 1 - k; };
-    double2 f0 = T2[1], f1 = T2[2], f2 = T2[3], f3 = T2[4];
-    double2 b0 = T2[bidx(0)], b1 = T2[bidx(1)], b2 = T2[bidx(2)], b3 = T2[bidx(3)];
+    double2 f0 = S2[1], f1 = S2[2], f2 = S2[3], f3 = S2[4];
     int k = 0;
     for (; k + 4 <= steps; k += 4) {
-      const double2 nf0 = T2[k + 5], nf1 = T2[k + 6], nf2 = T2[k + 7], nf3 = T2[k + 8];
-      const double2 nb0 = T2[bidx(k + 4)], nb1 = T2[bidx(k + 5)], nb2 = T2[bidx(k + 6)], nb3 = T2[bidx(k + 7)];
-      double sg[4], sq[4], sh[4], sr[4];
-      step(f0, b0);
-      sg[0] = fg1; sq[0] = fq; sh[0] = bg1; sr[0] = bq;
-      step(f1, b1);
-      sg[1] = fg1; sq[1] = fq; sh[1] = bg1; sr[1] = bq;
-      step(f2, b2);
-      sg[2] = fg1; sq[2] = fq; sh[2] = bg1; sr[2] = bq;
-      step(f3, b3);
+      const double2 n0 = S2[k + 5], n1 = S2[k + 6], n2 = S2[k + 7], n3 = S2[k + 8];
+      double sg[4], sq[4];
+      step(f0);
+      sg[0] = g1; sq[0] = qv;
+      step(f1);
+      sg[1] = g1; sq[1] = qv;
+      step(f2);
+      sg[2] = g1; sq[2] = qv;
+      step(f3);
       rescale_values();
-      sg[3] = fg1; sq[3] = fq; sh[3] = bg1; sr[3] = bq;
-      if (lane == 0) {
+      sg[3] = g1; sq[3] = qv;
+      if (wr) {
+        const int ib = i0 + di * k;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          gq[k + 1 + u] = sg[u];
-          gq[MMAX + k + 1 + u] = sq[u];
-          hr[m - 2 - k - u] = sh[u];
-          hr[MMAX + m - 2 - k - u] = sr[u];
+          v[ib + di * u] = sg[u];
+          v[MMAX + ib + di * u] = sq[u];
         }
         const int b = 2 * ((k + 4) >> 2);
-        exf[b] = static_cast<double>(feg);
-        exf[b + 1] = static_cast<double>(feq);
-        exb[b] = static_cast<double>(beg);
-        exb[b + 1] = static_cast<double>(beq);
+        exs[b] = static_cast<double>(eg);
+        exs[b + 1] = static_cast<double>(eq);
       }
-      f0 = nf0; f1 = nf1; f2 = nf2; f3 = nf3;
-      b0 = nb0; b1 = nb1; b2 = nb2; b3 = nb3;
+      f0 = n0; f1 = n1; f2 = n2; f3 = n3;
     }
     if (k < steps) {
-      step(f0, b0);
-      put(gq, k + 1, fg1, fq);
-      put(hr, m - 2 - k, bg1, bq);
+      step(f0);
+      if (wr) { v[i0 + di * k] = g1; v[MMAX + i0 + di * k] = qv; }
     }
     if (k + 1 < steps) {
-      step(f1, b1);
-      put(gq, k + 2, fg1, fq);
-      put(hr, m - 3 - k, bg1, bq);
+      step(f1);
+      if (wr) { v[i0 + di * (k + 1)] = g1; v[MMAX + i0 + di * (k + 1)] = qv; }
     }
     if (k + 2 < steps) {
-      step(f2, b2);
-      put(gq, k + 3, fg1, fq);
-      put(hr, m - 4 - k, bg1, bq);
+      step(f2);
+      if (wr) { v[i0 + di * (k + 2)] = g1; v[MMAX + i0 + di * (k + 2)] = qv; }
     }
   }
   wsym::lds_order();   // every lane reads its neighbours' chain values
@@ -584,7 +564,8 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
   double* zd = scr;
   double* tb = scr + wsym::kZd;
   double* trw = scr + kWScr;                      // [kWTrw] tridiagonal record
-  double* zbuf = trw + kWTrw;                     // [2][MMAX] eigenvectors of T (current / best check)
+  double* trev = trw + kWTrw;                     // [kWTrw] the record reversed (wave_check)
+  double* zbuf = trev + kWTrw;                    // [MMAX] eigenvector of T_m of the last check
   const int lane = threadIdx.x;
   const int r0 = 2 * lane, r1 = r0 + 1;
   const int n = A.n;
@@ -662,7 +643,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
 
       // ---- top eigenpair of M = W^1/2 C W^1/2 by plain Lanczos
       double lam = 0.0, resid = 0.0;
-      int m_conv = 0, nchecks = 0, zcur = 0, zbest = 0, m_retry = 0;
+      int m_conv = 0, nchecks = 0, m_retry = 0;
       bool converged = false;
       double tscale = 0.0;
       long long tcheck = 0, tmv = 0, tstep = 0, tph[4] = {0, 0, 0, 0};
@@ -848,7 +829,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
             const long long tc0 = dbg ? clock64() : 0;
             double lm, zl;
             int rounds = 0;
-            wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf + zcur * MMAX, scr, &lm, &zl, &rounds,
+            wave_check(trw, m, theta_lb, hint, glo, ghi, zbuf, scr, trev, &lm, &zl, &rounds,
                        dbg ? tph : nullptr);
             if (dbg) {
               tcheck += clock64() - tc0;
@@ -862,15 +843,12 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
               m_conv = m;
               lam = lm;
               resid = res;
-              zbest = zcur;
               break;
             }
             if (res < res_best) {
               m_pre = m_last;
               res_best = res;
               lam_best = lm;
-              zbest = zcur;
-              zcur ^= 1;
             }
             ghost = !reorth && res_best < 1e-13 * fabs(lam_best) && res > 4.0 * res_best;
             const bool out_of_steps = j == MMAX;
@@ -911,7 +889,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       // ---- Ritz vector u = V z of the accepted check
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // also orders the check's z writes before the reads
       {
-        const double* zb = zbuf + zbest * MMAX;
+        const double* zb = zbuf;   // the accepted check's (the last one)
         const double2* V2 = reinterpret_cast<const double2*>(Vb);
         // eight basis rows in flight per batch (the scratch is in L2 / the
         // Infinity Cache: one load latency per batch, not per row)

@@ -68,42 +68,6 @@ struct Packed {
   double cv[KV][2];
 };
 
-// AGPR parking of the VGPR part of the matrix around register-hungry code
-// that does not touch it (the tridiagonal check): the values move to the
-// accumulation registers (v_accvgpr_write, one VALU op per dword) and back, so
-// the allocator can hand their VGPRs to that code instead of spilling the
-// solver's state to scratch memory.  The asm statements are volatile and
-// ordered, so no use of P can move in between.
-template <int KV>
-struct Parked {
-  unsigned a[KV][4];
-};
-template <int KV>
-__device__ __forceinline__ void park(const Packed<KV>& P, Parked<KV>& Q) {
-#pragma unroll
-  for (int k = 0; k < KV; ++k) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const unsigned long long b = __builtin_bit_cast(unsigned long long, P.cv[k][s]);
-      asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(Q.a[k][2 * s]) : "v"(static_cast<unsigned>(b)));
-      asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(Q.a[k][2 * s + 1]) : "v"(static_cast<unsigned>(b >> 32)));
-    }
-  }
-}
-template <int KV>
-__device__ __forceinline__ void unpark(Packed<KV>& P, const Parked<KV>& Q) {
-#pragma unroll
-  for (int k = 0; k < KV; ++k) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      unsigned lo, hi;
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(Q.a[k][2 * s]));
-      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(hi) : "a"(Q.a[k][2 * s + 1]));
-      P.cv[k][s] = __builtin_bit_cast(double, (static_cast<unsigned long long>(hi) << 32) | lo);
-    }
-  }
-}
-
 // C[m][(m+k) mod 128] of diagonal k for this lane's two rows
 template <int KV, int K>
 __device__ __forceinline__ double2 diag(const Packed<KV>& P, const double* __restrict__ cl, int lane) {
