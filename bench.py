@@ -213,7 +213,7 @@ KERNEL_NAME = {
     "trimmedmean": "select_plain_kernel<1, 128, 12>",
     "median": "select_reg_kernel<128, 0, 128>",
     "average": "average_vec4_kernel",
-    "krum": "whole krum op (bf16x3 gram_pipe_kernel dominant; per-kernel split in profiles/)",
+    "krum": "whole krum op (bf16x3 gram_glds_kernel dominant; per-kernel split in profiles/)",
     "mom_krum": "whole mom_krum op (gram_bucket_kernel: bucket means fused into the bf16x3 Gram + scoring)",
     "bulyankrum": "whole bulyan op (bf16x3 Gram + theta Krum rounds + final stage)",
     "bulyanmedian": "whole bulyan op (theta fused select+distance rounds + final stage)",

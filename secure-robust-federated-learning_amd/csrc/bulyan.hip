@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(64) bulyan_listed_kernel(const float* __restri
 // value decides, as np.argmin does.  Columns failing the span test, or
 // holding a NaN or an infinity, go to bulyan_listed_kernel.
 template <int P>  // theta in (P - 16, P]
-__global__ void __launch_bounds__(256, P <= 48 ? 4 : (P <= 96 ? 2 : 1)) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
+__global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(const float* __restrict__ S, int64_t lds_,
                                                            const int* __restrict__ rows, int nrows_s, int theta,
                                                            int keep,
                                                            int64_t d, double* __restrict__ out,
@@ -790,15 +790,9 @@ __global__ void __launch_bounds__(256, P <= 48 ? 4 : (P <= 96 ? 2 : 1)) bulyan_f
   const bool even = (theta & 1) == 0;
   float cl, cu;            // centre candidates: the two middle values (even theta) or the median (cl)
   bool nonfinite = false;
-  // the column in selection order, kept for the even-theta tie-break (round 5:
-  // the re-read it replaces missed L2 -- 2x the algorithmic bytes -- and
-  // doubled the row-address SALU work; two waves per SIMD hold both copies)
-  float o[P2];
   {
     float v[P2];
     load_col(v, nonfinite);
-#pragma unroll
-    for (int i = 0; i < P; ++i) o[i] = v[i];
     if (__builtin_amdgcn_ballot_w64(nonfinite) != 0) {
 #pragma unroll
       for (int i = 0; i < P; ++i) v[i] = __builtin_isnan(v[i]) ? __builtin_inff() : v[i];
@@ -866,8 +860,18 @@ __global__ void __launch_bounds__(256, P <= 48 ? 4 : (P <= 96 ? 2 : 1)) bulyan_f
     if (keep == 0) result = __builtin_nan("");   // mean of an empty slice
     else if (even && cu != cl) tie = true;
     if (__builtin_amdgcn_ballot_w64(write && tie) != 0) {   // wave-uniform: every lane active
-      // even theta, two distinct middle values: np.argmin over the totals,
-      // from the column kept in selection order
+      // even theta, two distinct middle values: np.argmin over the totals.
+      // The row list is reloaded here, with every lane active, and kept opaque
+      // (the first gather's row addresses are then not held live for reuse)
+#pragma unroll
+      for (int q = 0; q < RW; ++q) {
+        const int li = 64 * q + t;
+        rl[q] = rows[li < theta ? li : theta - 1];
+        asm volatile("" : "+v"(rl[q]));
+      }
+      float o[P2];
+      bool dummy = false;
+      load_col(o, dummy);
       int fl = theta, fu = theta;
 #pragma unroll
       for (int i = P - 1; i >= 0; --i) {

@@ -22,13 +22,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOMINANT = {"trimmedmean": "select_plain_kernel", "median": "select_reg_kernel", "average": "average",
             "trimmedmean_n100": "select_plain_kernel", "median_n100": "select_reg_kernel",
             "trimmedmean_n512": "select_quad_kernel", "median_n512": "select_quad_kernel",
-            "krum": "gram_pipe_kernel", "dba_median": "select_reg_kernel", "dba_weighted_sum": "rows_vec4_kernel"}
+            "krum": "gram_glds_kernel", "dba_median": "select_reg_kernel", "dba_weighted_sum": "rows_vec4_kernel"}
 # Whole-op workloads (bench.py prices the whole call): traffic = the sum over
 # every sra:: dispatch of a call, the calls counted by one anchor launch each
 # (launches under 10 % of the largest anchor's fetch are bench.py's small
 # side calls, e.g. the solver-flop probe on 1000 columns, and are not counted)
 WHOLE_OP = {"filterl2": "chunk_gram", "ex_noregret": "chunk_gram", "mom_filterl2": "chunk_gram",
-            "mom_ex_noregret": "chunk_gram", "bulyankrum": "gram_partial_kernel", "mom_krum": "gram_bucket_kernel",
+            "mom_ex_noregret": "chunk_gram", "bulyankrum": "gram_glds_kernel", "mom_krum": "gram_bucket_kernel",
             "bulyanmedian": "bulyan_final", "bulyantrimmedmean": "bulyan_final"}
 
 
@@ -96,7 +96,10 @@ def main():
     tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
     for d in sorted(glob.glob(os.path.join(src, "pmc_*_FETCH_SIZE"))):
         name = re.match(r"pmc_(.*)_FETCH_SIZE", os.path.basename(d)).group(1)
-        line = bench_line(os.path.join(src, "%s.log" % name))
+        lp = os.path.join(src, "%s.log" % name)
+        line = bench_line(lp) if os.path.exists(lp) else None
+        if line is None:   # a PMC-only session: the bench line of the counter run itself
+            line = bench_line(os.path.join(src, "pmc_%s_FETCH_SIZE.log" % name))
         if line is None:
             continue
         cfg = line["config"]

@@ -28,6 +28,7 @@ mom_ex_noregret|--agg mom_ex_noregret --clients 512 --d 1.25e7 --steps 2"}
 PMC_WORKLOADS=${PMC_WORKLOADS:-"trimmedmean median average trimmedmean_n100 trimmedmean_n512 median_n512 krum"}
 while IFS='|' read -r name args; do
   [[ -z "$name" ]] && continue
+  [ -n "${SKIP_TRACE:-}" ] && continue
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUTD/$name" -o run \
     -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-host $args > "$OUTD/$name.log" 2>&1 \
     || { echo "trace $name failed rc=$?"; exit 1; }
