@@ -667,13 +667,24 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         for (int pass = 0; pass < 2; ++pass) {
           const double nb2 = wave_sum(n0 * n0 + n1 * n1);
           double hn2 = 0.0;
+          // the next block's loads are issued before this block's reduction
+          // (the basis is in the Infinity Cache: one latency per pass, not per block)
+          double2 raw[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) raw[u] = V2[(u < j ? u : 0) * 64 + lane];
           for (int qb = 0; qb <= j; qb += 8) {
             double2 v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const int q = qb + u;
-              const double2 b = V2[(q < j ? q : 0) * 64 + lane];
-              v[u] = q < j ? b : (q == j ? double2{q0, q1} : double2{0.0, 0.0});
+              v[u] = q < j ? raw[u] : (q == j ? double2{q0, q1} : double2{0.0, 0.0});
+            }
+            if (qb + 8 <= j) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int q = qb + 8 + u;
+                raw[u] = V2[(q < j ? q : 0) * 64 + lane];
+              }
             }
             double p[8], h[8];
 #pragma unroll
