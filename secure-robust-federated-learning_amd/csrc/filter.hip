@@ -1733,10 +1733,6 @@ size_t filter_workspace_bytes(int n, int64_t d, int itv, bool bucketed) {
          (bucketed ? static_cast<size_t>(n) * b * itv * sizeof(float) + 256 : 0);
 }
 
-// unused dynamic LDS of the bucket Gram: two blocks per CU instead of four
-// (each block streams 4 x 128 client rows at once)
-constexpr size_t kBucketGramPad = 40000;
-
 // bs > 0: the MoM forms -- X holds nsrc clients, n = the bucket count (<= FNP)
 int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int itv, double eps, double sigma,
                   double expansion, double* out, int* status, double* dbg, int* trace, void* ws, size_t ws_bytes,
@@ -1776,7 +1772,7 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     const int vec4 = bs > 0 && ldx % 4 == 0 && itv % 4 == 0 && d % 4 == 0 && ldb % 4 == 0 &&
                      (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(Bws) & 15) == 0;
     GramArgs ga{X, n, d, ldx, itv, c0, nb, Gws, bs, nsrc, Bws, ldb, vec4};
-    if (bs > 0) hipLaunchKernelGGL(chunk_gram_kernel<true>, dim3(nb), dim3(256), kBucketGramPad, s, ga);
+    if (bs > 0) hipLaunchKernelGGL(chunk_gram_kernel<true>, dim3(nb), dim3(256), 0, s, ga);
     else hipLaunchKernelGGL(chunk_gram_kernel<false>, dim3(nb), dim3(256), 0, s, ga);
     int rc = launch_status("chunk_gram_kernel");
     if (rc) return rc;

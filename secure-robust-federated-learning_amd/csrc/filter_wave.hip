@@ -733,9 +733,9 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
         // eps (beta_{k+1} + beta_{j+1}) / beta_{j+1}; omega_{j+1,j} = eps sqrt(n) |T| /
         // beta_{j+1}.  Returns max_k<=j |omega_{j+1,k}| and shifts the rows.
         auto omega_step = [&](int j, double aj, double bj, double bn, double tn) -> double {
-          const int up = (lane + 1) & 63, dn = (lane + 63) & 63;
-          const double u0 = __shfl(oc[0], up), u1 = __shfl(oc[1], up);
-          const double d0 = __shfl(oc[0], dn), d1 = __shfl(oc[1], dn);
+          // neighbours by DPP wave rotations (no LDS round trip)
+          const double u0 = wsym::rol1(oc[0]), u1 = wsym::rol1(oc[1]);
+          const double d0 = wsym::ror1(oc[0]), d1 = wsym::ror1(oc[1]);
           const double kp[2] = {lane < 63 ? u0 : u1, lane < 63 ? u1 : 0.0};
           const double km[2] = {lane > 0 ? d0 : 0.0, lane > 0 ? d1 : d0};
           const double ibn = 1.0 / bn;

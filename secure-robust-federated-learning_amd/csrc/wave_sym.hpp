@@ -48,6 +48,14 @@ __device__ __forceinline__ void sfor(F&& f) {
 // this.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
+// lane l + 1's value (lane 63 takes lane 0): DPP wave_rol:1
+__device__ __forceinline__ double rol1(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b), 0x134, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), 0x134, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
 // lane l - 1's value (lane 0 takes lane 63)
 __device__ __forceinline__ double ror1(double v) {
   const long long b = __builtin_bit_cast(long long, v);
