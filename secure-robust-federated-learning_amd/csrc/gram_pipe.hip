@@ -9,182 +9,20 @@
 
 namespace sra {
 
-// Software-pipelined Gram for 96 < N <= 128 (NB = 4, four waves, the C3
-// shape).  Same arithmetic as gram_body<4, 4, VEC, 0, 1, true> (per-wave means
-// from a fixed butterfly, the exact three-way split, six bf16 MFMAs per tile
-// and k-step, tiles accumulated in the same k order), scheduled so that the
-// MFMA pipe is never left idle while the wave does its VALU work: each of the
-// 60 MFMAs of a k-step is followed by one small piece of the NEXT k-step's
+// Software-pipelined Gram for N = 128 (NB = 4, four waves, the C3 shape).
+// Same arithmetic as gram_body<4, 4, VEC, 0, 1, true> (per-wave means from a
+// fixed butterfly, the exact three-way split, six bf16 MFMAs per tile and
+// k-step, tiles accumulated in the same k order), scheduled so that the MFMA
+// pipe is never left idle while the wave does its VALU work: each of the 60
+// MFMAs of a k-step is followed by one small piece of the NEXT k-step's
 // preparation (its LDS reads, the column sums and butterfly, the centring and
-// split of one element pair) or of the stage traffic (one ds_write_b128 of the
-// next stage, one global load of the stage after), pinned in place by
-// sched_barrier.  Stage s:
-//   phase A: MFMA(k-step g0 of s) | prepare g1 of s (LDS s)   | store s+1 -> LDS
-//   barrier
-//   phase B: MFMA(k-step g1 of s) | prepare g0 of s+1 (LDS s+1) | load s+2
-// One barrier per stage: buffer s&1 is last read in phase A of stage s and next
-// written in phase A of stage s+1; buffer (s+1)&1 is written in phase A of s and
-// first read after the barrier.
+// split of one element pair) or of the stage traffic, pinned in place by
+// sched_barrier.  (Rounds 3-4 staged each 128-coordinate stage through 64
+// VGPRs of register loads and a ds_write pass, one stage in flight per CU;
+// round 5 replaced that with the LDS-DMA ring below, bit-identical.)
 struct GramOps {
   bf16x8 h[4], m[4], l[4];
 };
-
-// Host contract (launch_gram_nbw<..., PIPE>): N == 128, 16-byte aligned rows,
-// d a multiple of the 128-coordinate stage, so every load is a full, guard-free
-// float4 and the loop body is one basic block (no branch for sched_barrier to
-// stop at); past the last stage the loads re-read the last stage (discarded).
-__device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
-                                               float* __restrict__ slab, float* lds) {
-  using C = GramCfg<4, 4, 0>;
-  constexpr int STAGE = C::STAGE;   // 128
-  constexpr int T = C::T;           // 10
-  static_assert(C::WK == 4 && C::KPW == 2 && C::LOADS == 16 && T == 10, "pipe layout");
-  auto bufp = [&](int which) { return lds + which * C::BUF; };
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int kg = tid >> 6;
-  const int64_t ntiles = d / STAGE;
-  const int nstage = blockIdx.x < ntiles ? static_cast<int>(cdiv(ntiles - blockIdx.x, gridDim.x)) : 0;
-  const float inv_n = 1.0f / static_cast<float>(n);
-  const int r = lane & 31;
-  const int h = lane >> 5;
-
-  f32x16 acc[T];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-
-  f32x4 stg[C::LOADS];
-  const int c4 = tid % C::C4;
-  const int row0 = tid / C::C4;
-  const uint32_t lane_off = static_cast<uint32_t>((static_cast<int64_t>(row0) * ldx + 4 * c4) * 4);
-  auto stage_k = [&](int s) {
-    return (static_cast<int64_t>(s < nstage ? s : nstage - 1) * gridDim.x + blockIdx.x) * STAGE;
-  };
-  auto load_one = [&](int64_t kb, int q) {
-    const char* bq = reinterpret_cast<const char*>(X + static_cast<int64_t>(C::RSTEP * q) * ldx + kb);
-    stg[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(bq + lane_off));
-  };
-  auto store_one = [&](float* b, int q) {
-    *reinterpret_cast<f32x4*>(b + (row0 + C::RSTEP * q) * C::ROWPAD + 4 * c4) = stg[q];
-  };
-
-  // preparation of one k-step, split in 43 pieces
-  f32x4 raw0[4], raw1[4], mu0, mu1;
-  auto prep_piece = [&](auto pc, const float* b, int g, GramOps& o) {
-    constexpr int p = decltype(pc)::value;
-    const int col = 16 * g + 8 * h;
-    if constexpr (p < 4) {
-      const float* rp = b + (32 * p + r) * C::ROWPAD + col;
-      raw0[p] = *reinterpret_cast<const f32x4*>(rp);
-      raw1[p] = *reinterpret_cast<const f32x4*>(rp + 4);
-    } else if constexpr (p == 4) {   // scalar adds: packed f32 VALU is slow beside MFMAs
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mu0[e] = ((raw0[0][e] + raw0[1][e]) + raw0[2][e]) + raw0[3][e];
-    } else if constexpr (p == 5) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mu1[e] = ((raw1[0][e] + raw1[1][e]) + raw1[2][e]) + raw1[3][e];
-    } else if constexpr (p < 26) {
-      // butterfly: level-major, two of the eight values per piece
-      constexpr int q = p - 6;          // 0..19
-      constexpr int lvl = q / 4;        // 0..4
-      constexpr int v0 = 2 * (q % 4);   // values v0, v0 + 1 of (mu0, mu1)
-#pragma unroll
-      for (int vv = v0; vv < v0 + 2; ++vv) {
-        float x = vv < 4 ? mu0[vv] : mu1[vv - 4];
-        int xi = __builtin_bit_cast(int, x);
-        int yi;
-        if constexpr (lvl == 0) yi = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
-        else if constexpr (lvl == 1) yi = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
-        else if constexpr (lvl == 2) yi = __builtin_amdgcn_ds_swizzle(xi, 0x101f);
-        else if constexpr (lvl == 3) yi = __builtin_amdgcn_ds_swizzle(xi, 0x201f);
-        else yi = __builtin_amdgcn_ds_swizzle(xi, 0x401f);
-        x += __builtin_bit_cast(float, yi);
-        if (vv < 4) mu0[vv] = x; else mu1[vv - 4] = x;
-      }
-    } else if constexpr (p == 26) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        mu0[e] = mu0[e] * inv_n;
-        mu1[e] = mu1[e] * inv_n;
-      }
-    } else if constexpr (p < 43) {
-      // centre + split one element pair of one block
-      constexpr int blk = (p - 27) / 4;
-      constexpr int e2 = (p - 27) % 4;
-      float x0 = e2 < 2 ? raw0[blk][2 * e2] - mu0[2 * e2] : raw1[blk][2 * e2 - 4] - mu1[2 * e2 - 4];
-      float x1 = e2 < 2 ? raw0[blk][2 * e2 + 1] - mu0[2 * e2 + 1] : raw1[blk][2 * e2 - 3] - mu1[2 * e2 - 3];
-      uint32_t hb, mb, lb;
-      split3_pair(x0, x1, hb, mb, lb);
-      set_pair(o.h[blk], e2, hb);
-      set_pair(o.m[blk], e2, mb);
-      set_pair(o.l[blk], e2, lb);
-    }
-  };
-  auto mfma_slot = [&](auto ic, const GramOps& o) {
-    constexpr int i = decltype(ic)::value;
-    constexpr int t = i / 6, term = i % 6;
-    constexpr int ti = C::kTileI(t), tj = C::kTileJ(t);
-    if constexpr (term == 0) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.h[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 1) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.m[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 2) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.m[ti], o.h[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 3) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.h[ti], o.l[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 4) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.l[ti], o.h[tj], acc[t], 0, 0, 0);
-    if constexpr (term == 5) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.m[ti], o.m[tj], acc[t], 0, 0, 0);
-  };
-
-  GramOps opA, opB;
-  if (nstage > 0) {
-#pragma unroll
-    for (int q = 0; q < C::LOADS; ++q) load_one(stage_k(0), q);
-#pragma unroll
-    for (int q = 0; q < C::LOADS; ++q) store_one(bufp(0), q);
-#pragma unroll
-    for (int q = 0; q < C::LOADS; ++q) load_one(stage_k(1), q);
-    __syncthreads();
-    static_for<0, 43>([&](auto pc) { prep_piece(pc, bufp(0), kg, opA); });
-  }
-
-  for (int s = 0; s < nstage; ++s) {
-    const float* b = bufp(s & 1);
-    float* bn = bufp((s + 1) & 1);
-    // phase A (past the last stage the store writes a copy of the last stage
-    // into the free buffer: nobody reads it)
-    const int64_t k2 = stage_k(s + 2);
-    static_for<0, 60>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      mfma_slot(ic, opA);
-      if constexpr (i < 43) {
-        prep_piece(ic, b, kg + 4, opB);
-      } else if constexpr (i < 59) {
-        store_one(bn, i - 43);
-        load_one(k2, i - 43);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    __syncthreads();
-    // phase B
-    static_for<0, 60>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      mfma_slot(ic, opB);
-      if constexpr (i < 43) prep_piece(ic, bn, kg, opA);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-
-  float* my = slab + (static_cast<int64_t>(blockIdx.x) * C::WK + kg) * T * 1024;
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    float* o = my + t * 1024;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      o[row * 32 + r] = acc[t][reg];
-    }
-  }
-}
 
 // ---- round 5: the same pipeline with LDS-DMA staging ----------------------
 // global_load_lds_dwordx4 writes a stage straight into LDS (no VGPR landing
@@ -194,7 +32,8 @@ __device__ __forceinline__ void gram_body_pipe(const float* __restrict__ X, int 
 // per CU) are in flight instead of one 64 KiB stage.  One k-step per wave per
 // stage; a block walks the same coordinates in the same order as the 128-wide
 // pipe (64-stage t = half t & 1 of 128-stage t >> 1), so every wave
-// accumulates the same k-steps in the same order: the Gram is bit-identical.
+// accumulates the same k-steps in the same order: the Gram is bit-identical
+// to the register-staged kernel it replaced.
 //
 // LDS image: lane-linear per instruction (64 lanes x 16 B = four 256-byte
 // rows), the 16-byte chunks of row r XOR-swizzled by r & 15 (conflict-free
@@ -214,7 +53,7 @@ __device__ __forceinline__ void gram_body_glds(const float* __restrict__ X, int 
   constexpr int T = C::T;   // 10
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int kg = tid >> 6;
+  const int kg = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the DMA row-block bases in SGPRs
   const int64_t ntiles = d / 128;
   const int nstage = blockIdx.x < ntiles ? static_cast<int>(cdiv(ntiles - blockIdx.x, gridDim.x)) : 0;
   const int nst = 2 * nstage;   // 64-wide stages
@@ -370,33 +209,16 @@ __global__ void __launch_bounds__(256) gram_glds_kernel(const float* __restrict_
   gram_body_glds(X, n, d, ldx, slab, lds);
 }
 
-// the next-but-one stage's loads are issued in phase A right behind the
-// stores, 1.5 phases ahead of their use (phase-B loads measured 1.53 vs 1.48 ms)
-__global__ void __launch_bounds__(256) gram_pipe_kernel(const float* __restrict__ X, int n, int64_t d, int64_t ldx,
-                                                        float* __restrict__ slab) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  gram_body_pipe(X, n, d, ldx, slab, lds);
-}
-
-constexpr bool kGramGlds = true;   // LDS-DMA staging (round 5) vs register staging
-
 int launch_gram_pipe(const float* X, int n, int64_t d, int64_t ldx, float* slab, int nwg, hipStream_t s) {
   using C = GramCfg<4, 4, 0>;
   SRA_REQUIRE(n == 128 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 && d % C::STAGE == 0,
               SRA_ERR_ARG, "pipelined Gram needs N == 128, aligned rows and d %% %d == 0", C::STAGE);
   SRA_REQUIRE(gram_pipe_offsets_fit(ldx), SRA_ERR_ARG,
               "pipelined Gram: the 32-bit lane offsets cannot address rows %lld floats apart", (long long)ldx);
-  if (kGramGlds) {
-    const size_t lds = sizeof(float) * 4 * kGldsBuf;
-    SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_glds_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    hipLaunchKernelGGL(gram_glds_kernel, dim3(nwg), dim3(256), lds, s, X, n, d, ldx, slab);
-    return SRA_OK;
-  }
-  const size_t lds = sizeof(float) * 2 * C::BUF;
-  SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_pipe_kernel),
+  const size_t lds = sizeof(float) * 4 * kGldsBuf;
+  SRA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_glds_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-  hipLaunchKernelGGL(gram_pipe_kernel, dim3(nwg), dim3(256), lds, s, X, n, d, ldx, slab);
+  hipLaunchKernelGGL(gram_glds_kernel, dim3(nwg), dim3(256), lds, s, X, n, d, ldx, slab);
   return SRA_OK;
 }
 

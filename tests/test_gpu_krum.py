@@ -66,7 +66,7 @@ def test_gram_matches_fp64(n):
 @pytest.mark.parametrize("k", [1, 5, 257, 600])
 def test_gram_n128_whole_stages(k):
     """N = 128 with d a multiple of the 128-coordinate stage: the software-
-    pipelined Gram (gram_pipe_kernel) when selected; workgroups with 0, 1, 2 and
+    pipelined Gram (gram_glds_kernel) when selected; workgroups with 0, 1, 2 and
     3 stages; identical rows keep distance exactly 0."""
     n, d = 128, 128 * k
     x = make_rows(n, d, seed=900 + k, byz=8, identical_byz=True)

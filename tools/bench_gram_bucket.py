@@ -2,7 +2,7 @@
 
   python tools/bench_gram_bucket.py            (on the GPU box)
 
-N = 128 x 1e7 (C3): engine.gram (gram_pipe_kernel) vs engine.gram_buckets(X, 1)
+N = 128 x 1e7 (C3): engine.gram (gram_glds_kernel) vs engine.gram_buckets(X, 1)
 (the same kernel family as mom_krum's, bucket size 1); N = 171/200 plain; the
 C5 mom_krum shape (512 x 1.25e7, buckets of 3) fused vs bucket means + Gram.
 Prints ms per call (HIP events, median of 10) and max |dG| / max|G| between
