@@ -64,7 +64,7 @@ def test_dual_oracle_trace_and_bound(rec):
         assert err <= rec["bound"][c]
 
 
-@pytest.mark.parametrize("name", ["trace_filterL2_c4", "trace_ex_noregret_c4"])
+@pytest.mark.parametrize("name", [pytest.param("trace_filterL2_c4", marks=pytest.mark.slow), "trace_ex_noregret_c4"])
 def test_primal_oracle_full_trace(name):
     """The primal (k x k LAPACK) oracle reproduces every decision of the C4
     chunks exactly, iteration count included."""
