@@ -1047,6 +1047,7 @@ __global__ void __launch_bounds__(256) chunk_mean_kernel(const float* __restrict
   const int64_t j = j0 + static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (j >= j1) return;
   const int b = static_cast<int>((j - j0) / itv);
+  if (cs == FNP && misc[static_cast<size_t>(b) * kMisc + 3] != 0.0) return;   // written by wave_solve_kernel
   const double* cb = c + static_cast<size_t>(b) * cs;
   const int* ab = act + static_cast<size_t>(b) * cs;
   if (unw && misc[static_cast<size_t>(b) * kMisc + 2] != 0.0) {
@@ -1791,7 +1792,8 @@ int launch_filter(int mode, const float* X, int n, int64_t d, int64_t ldx, int i
     constexpr int first_off = -12;
     SolveArgs sa{Gws, cws, aws, mws, status, n, nb, eps, sigma, expansion, c0 == 0 ? dbg : nullptr, Vws, fbl, fbc,
                  trace != nullptr ? trace + static_cast<size_t>(c0) * kTraceStride : nullptr, first_off,
-                 kMaxAdvance, 0};
+                 kMaxAdvance, 0, bs > 0 ? Bws : X, bs > 0 ? ldb : ldx, bs > 0 ? c0 * itv : int64_t(0), itv, d, c0,
+                 out};
     SRA_HIP(hipMemsetAsync(fbc, 0, 8 * sizeof(int), s));
     const int lgrid = nb < lgrid_max ? nb : lgrid_max;
     // both filters on the one-wave solver (ex_noregret re-orthogonalising

@@ -112,9 +112,20 @@ struct SolveArgs {
   int* fb_list;      // chunks handed to the re-orthogonalising fallback
   int* fb_count;
   int* trace;        // optional [nb][1 + 2 FNP] decision trace (sra_filter_trace_f32), batch-relative
-  int first_off;     // lanczos_solve_kernel: first check at (previous iteration's steps) + first_off
-  int max_adv;       // lanczos_solve_kernel: checks at most this many steps apart
-  int warm;          // lanczos_solve_kernel, ex_noregret: warm start from the previous Ritz vector
+  int first_off;     // first check at (previous iteration's steps) + first_off
+  int max_adv;       // checks at most this many steps apart
+  int warm;          // (unused since round 5)
+  // round 5: wave_solve_kernel writes the chunk means itself once a chunk's
+  // weights are final (chunk_mean_kernel's arithmetic and order) and flags the
+  // chunk in misc[kMisc * ch + 3]; chunk_mean_kernel then covers only the
+  // chunks the fallback solver finished.  Xm = X or the batch's bucket rows.
+  const float* Xm;
+  int64_t ldxm;
+  int64_t jx0;       // column of Xm holding the batch's first coordinate
+  int itv;
+  int64_t d;
+  int64_t chunk0;    // the batch's first chunk
+  double* out;
 };
 
 // Decision trace of one chunk (sra_filter_trace_f32): [0] iterations completed

@@ -556,6 +556,47 @@ __device__ bool wave_kl_project(double& c0, double& c1, bool ai0, bool ai1, int 
   return ok;
 }
 
+// out[j] = sum_i kept c_i x_ij / scale over the chunk's coordinates in fp64
+// with the clients in order (chunk_mean_kernel's arithmetic, bit-identical);
+// unweighted (ex_noregret's None exit): the fp32 mean.  cv / kf: the weights
+// and kept flags in LDS.  A lane per coordinate, sixteen per pass in flight.
+__device__ __attribute__((noinline)) void chunk_means(const float* Xm, int64_t ldxm, int64_t jx0, int64_t gj0, int itv,
+                                                      int64_t d, int n, const double* cv, const double* kf,
+                                                      double scale, bool unw, double* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gj1 = gj0 + itv < d ? gj0 + itv : d;
+  const int kk = static_cast<int>(gj1 - gj0);
+  const float* xb = Xm + (gj0 - jx0);
+  for (int jb = 0; jb < kk; jb += 16 * 64) {
+    double acc[16];
+    float acc32[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      acc[t] = 0.0;
+      acc32[t] = 0.f;
+    }
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) {
+      if (kf[i] == 0.0) continue;   // wave-uniform
+      const double ci = cv[i];
+      ++cnt;
+      const float* xr = xb + static_cast<int64_t>(i) * ldxm;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int jj = jb + 64 * t + lane;
+        const float x = jj < kk ? xr[jj] : 0.f;
+        if (unw) acc32[t] += x;
+        else acc[t] += static_cast<double>(x) * ci;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int jj = jb + 64 * t + lane;
+      if (jj < kk) out[gj0 + jj] = unw ? static_cast<double>(acc32[t] / static_cast<float>(cnt)) : acc[t] / scale;
+    }
+  }
+}
+
 template <int MODE, bool DBG>
 __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1020,6 +1061,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       if (lane == 0) {
         const int k = atomicAdd(A.fb_count, 1);
         A.fb_list[k] = ch;
+        A.misc[static_cast<size_t>(ch) * kMisc + 3] = 0.0;   // chunk_mean_kernel writes its means
       }
       continue;
     }
@@ -1039,17 +1081,27 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
       reinterpret_cast<double2*>(cv)[lane] = double2{c0, c1};
       reinterpret_cast<double2*>(kf)[lane] = double2{ai0 ? 1.0 : 0.0, ai1 ? 1.0 : 0.0};
       wsym::lds_order();
+      double scale = 0.0;
       if (lane == 0) {
         double* kept = tb + FNP;   // [FNP]
         int q2 = 0;
         for (int i = 0; i < n; ++i)
           if (kf[i] != 0.0) kept[q2++] = cv[i];
-        A.misc[static_cast<size_t>(ch) * kMisc] = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
+        scale = np_pw64(0, q2, [&](int zz) { return kept[zz]; });
+        A.misc[static_cast<size_t>(ch) * kMisc] = scale;
+        A.misc[static_cast<size_t>(ch) * kMisc + 3] = 1.0;   // the means below
         if constexpr (MODE == 1) {
           A.misc[static_cast<size_t>(ch) * kMisc + 2] = unweighted ? 1.0 : 0.0;
           if (unweighted) atomicAdd(A.status + 1, 1);
         }
       }
+      scale = readlane_f64(scale, 0);
+      wsym::lds_order();
+      // ---- the chunk's means (chunk_mean_kernel's arithmetic and order, so
+      // bit-identical), out of line: its accumulators do not widen the
+      // solver's register allocation
+      chunk_means(A.Xm, A.ldxm, A.jx0, (A.chunk0 + ch) * static_cast<int64_t>(A.itv), A.itv, A.d, n, cv, kf, scale,
+                  MODE == 1 && unweighted, A.out);
       wsym::lds_order();
     }
   }
