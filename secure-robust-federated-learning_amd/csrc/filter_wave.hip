@@ -913,7 +913,7 @@ __global__ void __launch_bounds__(64, 1) wave_solve_kernel(SolveArgs A) {
               m_retry = m_pre;
               break;
             }
-            int adv = 4;
+            int adv = 6;   // first interval, before a convergence rate is known (A/B: 4 -> 6 saves ~1 %, 8 loses 10 %)
             double rate = rate_hint;
             if (m_a >= 0 && res_a > res && res > 0.0) rate = rate_hint = log(res / res_a) / (m - m_a);
             if (rate < 0.0 && res > 0.0) {
