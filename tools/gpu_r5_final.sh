@@ -12,3 +12,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 "$OUT/smoke.log"
 timeout -k 10 300 python -u bench.py > "$OUT/bench_default.log" 2>&1 || { tail -5 "$OUT/bench_default.log"; exit 1; }
 tail -1 "$OUT/bench_default.log"
+# kernel stats + bench lines of the four spectral-filter workloads (gpurun_out/r5g/)
+W='filterl2|--agg filterl2 --d 1e7 --steps 3 --warmup 1
+ex_noregret|--agg ex_noregret --d 1e7 --steps 3 --warmup 1
+mom_filterl2|--agg mom_filterl2 --clients 512 --d 1.25e7 --steps 3 --warmup 1
+mom_ex_noregret|--agg mom_ex_noregret --clients 512 --d 1.25e7 --steps 3 --warmup 1' TAG=r5g bash tools/gpu_r5_prof.sh
