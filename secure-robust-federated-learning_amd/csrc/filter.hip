@@ -120,13 +120,25 @@ __device__ __forceinline__ void gram_tiles(const GramArgs& A, int64_t k0, int k,
         if (r < n && nvalid > 0) {
           const int lo = r * A.bs, hi = lo + A.bs < A.nsrc ? lo + A.bs : A.nsrc;
           float4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-          for (int q = lo; q < hi; ++q) {
-            const float4 x = *reinterpret_cast<const float4*>(A.X + static_cast<int64_t>(q) * A.ldx + colv);
+          auto add = [&](const float4 x) {
             acc.x += x.x;
             acc.y += x.y;
             acc.z += x.z;
             acc.w += x.w;
+          };
+          if (hi - lo == 4) {   // a full bucket of four: its loads issued together (C5 Gram 9.67 -> 9.30 ms)
+            const float* p = A.X + static_cast<int64_t>(lo) * A.ldx + colv;
+            const float4 x0 = *reinterpret_cast<const float4*>(p);
+            const float4 x1 = *reinterpret_cast<const float4*>(p + A.ldx);
+            const float4 x2 = *reinterpret_cast<const float4*>(p + 2 * A.ldx);
+            const float4 x3 = *reinterpret_cast<const float4*>(p + 3 * A.ldx);
+            add(x0);
+            add(x1);
+            add(x2);
+            add(x3);
+          } else {
+#pragma unroll 4
+            for (int q = lo; q < hi; ++q) add(*reinterpret_cast<const float4*>(A.X + static_cast<int64_t>(q) * A.ldx + colv));
           }
           const float cnt = static_cast<float>(hi - lo);
           v = float4{acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt};
