@@ -459,7 +459,7 @@ def main():
         ops = shard.engine_ops()
         dtot = d * world
         if a.agg == "krum":
-            sharded = lambda: shard.krum(ops["gram"], ops["krum_select"], X, dtot, 20)[0]
+            sharded = lambda: shard.krum(ops["gram"], ops["krum_select"], X, dtot, 20, exact=ops)[0]
         elif a.agg == "mom_krum":
             sharded = lambda: shard.mom_krum(ops, X, dtot, 20)[0]
         else:

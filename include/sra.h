@@ -123,6 +123,27 @@ int sra_krum_from_gram_workspace_bytes(int64_t n, size_t* bytes);
 int sra_krum_from_gram(const double* G, int64_t n, int32_t f, int32_t rounds, int32_t* order, float* scores,
                        void* ws, size_t ws_bytes, void* stream);
 
+/* Exact per-pair route over a column-sharded layer: the
+ * reference's np.linalg.norm(sample - sample_) (src/robust_estimator.py:242)
+ * squared is a sum over columns, so each rank's shard contributes
+ *   acc[i*nb + j] (i < j) = sum_k fp32(x_ik - x_jk)^2   (fp64)
+ * over its columns, class-coded in place: NaN when any term is NaN, else +inf
+ * when any is inf (fp64 addition of the ranks' partials keeps that class
+ * rule).  Rows are the n clients (bucket_size 1) or the means of consecutive
+ * buckets of bucket_size clients (np.mean order, mom_krum's rows); nb =
+ * ceil(n / bucket_size) <= 8192.  acc is nb x nb fp64 (only i < j written,
+ * the rest zeroed); ws from sra_krum_pair_sq_workspace_bytes. */
+int sra_krum_pair_sq_workspace_bytes(int64_t n, int32_t bucket_size, size_t* bytes);
+int sra_krum_pair_sq_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size, double* acc,
+                         void* ws, size_t ws_bytes, void* stream);
+
+/* The selection of sra_krum_from_gram from the summed class-coded pair sums
+ * of sra_krum_pair_sq_f32 (distance = sqrt(fp32(acc)), NaN sorted last in
+ * each row, first minimum score): the unsharded exact route's scoring. */
+int sra_krum_from_pairs_workspace_bytes(int64_t n, size_t* bytes);
+int sra_krum_from_pairs(const double* acc, int64_t n, int32_t f, int32_t rounds, int32_t* order, float* scores,
+                        void* ws, size_t ws_bytes, void* stream);
+
 /* out[r, :] = X[rows[r], :] for r < nrows (rows is a device int32 array of
  * indices into the n rows of X; an index outside [0, n) is clamped and counted,
  * see sra_row_fault_count). */

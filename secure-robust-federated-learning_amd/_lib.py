@@ -71,6 +71,10 @@ _SIGS = {
     "sra_krum_select_f32": [_ptr, _i64, _i64, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
     "sra_krum_from_gram_workspace_bytes": [_i64, ctypes.POINTER(_sz)],
     "sra_krum_from_gram": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
+    "sra_krum_pair_sq_workspace_bytes": [_i64, _i32, ctypes.POINTER(_sz)],
+    "sra_krum_pair_sq_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr, _sz, _ptr],
+    "sra_krum_from_pairs_workspace_bytes": [_i64, ctypes.POINTER(_sz)],
+    "sra_krum_from_pairs": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _sz, _ptr],
     "sra_gather_rows_f32": [_ptr, _i64, _i64, _i64, _ptr, _i32, _ptr, _i64, _ptr],
     "sra_gram_buckets_f32": [_ptr, _i64, _i64, _i64, _i32, _ptr, _ptr, _sz, _ptr],
     "sra_mom_krum_workspace_bytes": [_i64, _i64, _i32, ctypes.POINTER(_sz)],

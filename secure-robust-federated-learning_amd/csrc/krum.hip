@@ -150,7 +150,9 @@ __global__ void __launch_bounds__(256) krum_rowsort_kernel(const float* __restri
       const int j = p < i ? p : p + 1;
       if (direct) {
         const int64_t e = i < j ? (int64_t)i * n + j : (int64_t)j * n + i;
-        const int c = cls[e];
+        // (cls == nullptr: acc is class-coded itself, NaN / inf in place --
+        // the sharded route's summed partials, launch_krum_from_pairs)
+        const int c = cls != nullptr ? cls[e] : 0;
         // np.sqrt of the fp32 squared norm (inf on fp32 overflow)
         kv[p] = (c & 1) ? __builtin_nanf("") : (c & 2) ? __builtin_inff() : sqrtf(static_cast<float>(acc[e]));
       } else {
@@ -542,6 +544,9 @@ size_t krum_workspace_bytes(int n, int64_t d) {
   return 256 + nn * 8 * 2 + nn * 4 * 4 + krum_scratch_bytes(n) + gram_workspace_bytes(n, d);
 }
 
+static int launch_rowsort_and_rounds(const float* D, int n, int f, int rounds, int* order, float* scores0,
+                                     const int* nonfinite, const double* acc, const int* cls, hipStream_t s);
+
 // X (optional): the data G came from; with it, a non-finite G switches the
 // distances to the exact per-pair route (krum_direct_kernel), nonfinite / acc
 // its flag and n x n fp64 accumulator
@@ -550,8 +555,7 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
                               hipStream_t s, int nx = 0, int bs = 1) {
   const size_t nn = static_cast<size_t>(n) * n;
   float* D = reinterpret_cast<float*>(ws);
-  float* S = D + nn;
-  int* J = reinterpret_cast<int*>(S + nn);
+  (void)nn;
   // narrow layers (d <= kExactMaxD) always take the exact route: with few
   // coordinates the nearest pairs sit far below the rows' norms, where the
   // Gram's G_ii + G_jj - 2 G_ij loses the bits the reference's fp32 norm of
@@ -571,6 +575,18 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
     rc = launch_status("krum_direct_kernel");
     if (rc) return rc;
   }
+  return launch_rowsort_and_rounds(D, n, f, rounds, order, scores0, X ? nonfinite : nullptr, X ? acc : nullptr,
+                                   X ? cls : nullptr, s);
+}
+
+// Row sorts and the selection rounds, from D (or, with *nonfinite set, from the
+// exact per-pair acc / cls); D heads [D n*n][S n*n][J n*n][rounds scratch].
+static int launch_rowsort_and_rounds(const float* D, int n, int f, int rounds, int* order, float* scores0,
+                                     const int* nonfinite, const double* acc, const int* cls, hipStream_t s) {
+  const size_t nn = static_cast<size_t>(n) * n;
+  float* S = const_cast<float*>(D) + nn;
+  int* J = reinterpret_cast<int*>(S + nn);
+  int rc = SRA_OK;
   if (n > 1) {
     int pn = 1;
     while (pn < n - 1) pn <<= 1;
@@ -579,8 +595,7 @@ static int launch_krum_rounds(const double* G, int n, int f, int rounds, int* or
                             hipFuncAttributeMaxDynamicSharedMemorySize, 8 * kKrumMaxClients);
     SRA_REQUIRE(attr_s == hipSuccess || pn * 8 <= 65536, SRA_ERR_UNSUPPORTED,
                 "krum_rowsort_kernel: cannot reserve %d bytes of dynamic LDS", pn * 8);
-    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), pn * 8, s, D, n, S, J, X ? nonfinite : nullptr,
-                       X ? acc : nullptr, X ? cls : nullptr);
+    hipLaunchKernelGGL(krum_rowsort_kernel, dim3(n), dim3(256), pn * 8, s, D, n, S, J, nonfinite, acc, cls);
     rc = launch_status("krum_rowsort_kernel");
     if (rc) return rc;
   }
@@ -692,9 +707,102 @@ int launch_mom_krum(const float* X, int n, int64_t d, int64_t ldx, int f, int bs
   return launch_status("bucket_row_kernel");
 }
 
+// ---------------------------------------------------------------------------
+// The exact per-pair route over a column-sharded layer (shard.krum, mom_krum,
+// Bulyan-Krum).  ||a - b||^2 over all columns is the sum over the
+// shards of ||a_s - b_s||^2, so every rank forms its partial with
+// krum_direct_kernel, codes the pair's class into the value (NaN if any term
+// is NaN, else +inf if any is inf: fp64 addition of the ranks' partials then
+// reproduces the reference's class rule, NaN + x = NaN, inf + finite = inf), one
+// reduce sums them on the scoring rank, and launch_krum_from_pairs scores the
+// sum with the unsharded route's row sort (NaN last) and rounds.
+// ---------------------------------------------------------------------------
+__global__ void pair_encode_kernel(double* __restrict__ acc, const int* __restrict__ cls, int n) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= static_cast<int64_t>(n) * n) return;
+  const int c = cls[e];
+  if (c & 1) acc[e] = __builtin_nan("");
+  else if (c & 2) acc[e] = __builtin_inf();
+}
+
+// [flag (256 B)][cls int n*n]
+size_t krum_pair_sq_workspace_bytes(int nb) { return 256 + static_cast<size_t>(nb) * nb * 4; }
+
+int launch_krum_pair_sq(const float* X, int nx, int64_t d, int64_t ldx, int bs, double* acc, void* ws,
+                        size_t ws_bytes, hipStream_t s) {
+  const int nb = static_cast<int>(cdiv(nx, bs));
+  SRA_REQUIRE(nb >= 1 && nb <= kKrumMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d (got %d)",
+              kKrumMaxClients, nb);
+  SRA_REQUIRE(ws != nullptr && ws_bytes >= krum_pair_sq_workspace_bytes(nb), SRA_ERR_WORKSPACE,
+              "pair workspace too small: need %zu bytes", krum_pair_sq_workspace_bytes(nb));
+  const size_t nn = static_cast<size_t>(nb) * nb;
+  int* flag = static_cast<int*>(ws);
+  int* cls = reinterpret_cast<int*>(static_cast<char*>(ws) + 256);
+  SRA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag), 1, 1, s));
+  SRA_HIP(hipMemsetAsync(acc, 0, nn * 8, s));
+  SRA_HIP(hipMemsetAsync(cls, 0, nn * 4, s));
+  if (nb > 1) {
+    const int nt = static_cast<int>(cdiv(nb, kDirTile));
+    const int64_t kb = cdiv(d, kDirK);
+    const int slices = d <= kExactMaxD ? 1 : static_cast<int>(kb < 256 ? kb : 256);
+    hipLaunchKernelGGL(krum_direct_kernel, dim3(slices, nt * (nt + 1) / 2), dim3(256), 0, s, X, nb, d, ldx,
+                       bs == 1 ? nb : nx, bs, flag, acc, cls, slices);
+    int rc = launch_status("krum_direct_kernel");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(pair_encode_kernel, dim3(cdiv(static_cast<int64_t>(nn), 256)), dim3(256), 0, s, acc, cls, nb);
+  return launch_status("pair_encode_kernel");
+}
+
+// [flag (256 B)][D n*n][S n*n][J n*n][rounds scratch]
+size_t krum_from_pairs_workspace_bytes(int n) { return 256 + krum_from_gram_workspace_bytes(n); }
+
+int launch_krum_from_pairs(const double* acc, int n, int f, int rounds, int* order, float* scores0, void* ws,
+                           hipStream_t s) {
+  int* flag = static_cast<int*>(ws);
+  SRA_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag), 1, 1, s));
+  return launch_rowsort_and_rounds(reinterpret_cast<float*>(static_cast<char*>(ws) + 256), n, f, rounds, order,
+                                   scores0, flag, acc, nullptr, s);
+}
+
 }  // namespace sra
 
 using namespace sra;
+
+extern "C" int sra_krum_pair_sq_workspace_bytes(int64_t n, int32_t bucket_size, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(bucket_size >= 1 && n >= 1 && cdiv(n, bucket_size) <= kKrumMaxClients, SRA_ERR_UNSUPPORTED,
+              "Krum supports 1 <= ceil(N / bucket size) <= %d", kKrumMaxClients);
+  *bytes = krum_pair_sq_workspace_bytes(static_cast<int>(cdiv(n, bucket_size)));
+  return SRA_OK;
+}
+
+extern "C" int sra_krum_pair_sq_f32(const float* X, int64_t n, int64_t d, int64_t ldx, int32_t bucket_size,
+                                    double* acc, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(X != nullptr && acc != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= (int64_t(1) << 30) && d >= 1 && ldx >= d, SRA_ERR_SHAPE, "bad shape");
+  SRA_REQUIRE(bucket_size >= 1, SRA_ERR_ARG, "bucket size must be >= 1 (got %d)", bucket_size);
+  return launch_krum_pair_sq(X, static_cast<int>(n), d, ldx, bucket_size, acc, ws, ws_bytes,
+                             static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sra_krum_from_pairs_workspace_bytes(int64_t n, size_t* bytes) {
+  SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");
+  SRA_REQUIRE(n >= 1 && n <= kKrumMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kKrumMaxClients);
+  *bytes = krum_from_pairs_workspace_bytes(static_cast<int>(n));
+  return SRA_OK;
+}
+
+extern "C" int sra_krum_from_pairs(const double* acc, int64_t n, int32_t f, int32_t rounds, int32_t* order,
+                                   float* scores, void* ws, size_t ws_bytes, void* stream) {
+  SRA_REQUIRE(acc != nullptr && order != nullptr && ws != nullptr, SRA_ERR_ARG, "null pointer");
+  SRA_REQUIRE(n >= 1 && n <= kKrumMaxClients, SRA_ERR_UNSUPPORTED, "Krum supports 1 <= N <= %d", kKrumMaxClients);
+  SRA_REQUIRE(rounds >= 1 && rounds <= n, SRA_ERR_ARG, "rounds must be in [1, N]");
+  SRA_REQUIRE(ws_bytes >= krum_from_pairs_workspace_bytes(static_cast<int>(n)), SRA_ERR_WORKSPACE,
+              "workspace too small: need %zu bytes", krum_from_pairs_workspace_bytes(static_cast<int>(n)));
+  return launch_krum_from_pairs(acc, static_cast<int>(n), f, rounds, order, scores, ws,
+                                static_cast<hipStream_t>(stream));
+}
 
 extern "C" int sra_mom_krum_workspace_bytes(int64_t n, int64_t d, int32_t bucket_size, size_t* bytes) {
   SRA_REQUIRE(bytes != nullptr, SRA_ERR_ARG, "null bytes pointer");

@@ -129,6 +129,33 @@ def krum_from_gram(G, f, rounds=1, scores=True):
     return order, sc
 
 
+def krum_pair_sq(X, bucket_size=1):
+    """Class-coded sums of squared fp32 differences over X's columns (nb x nb
+    float64, i < j; NaN / +inf where the reference's norm is NaN / inf) of the
+    clients (bucket_size 1) or of the means of consecutive buckets: one
+    shard's contribution to the sharded Krum family's exact route."""
+    X, n, d, ldx = as_matrix(X)
+    nb = -(-n // int(bucket_size))
+    A = torch.empty((nb, nb), dtype=torch.float64, device=X.device)
+    nbytes = _lib.query_bytes("sra_krum_pair_sq_workspace_bytes", n, int(bucket_size))
+    ws = _workspace(nbytes, X.device)
+    _lib.call("sra_krum_pair_sq_f32", X.data_ptr(), n, d, ldx, int(bucket_size), A.data_ptr(), ws.data_ptr(), nbytes,
+              _stream_ptr(X.device))
+    return A
+
+
+def krum_from_pairs(A, f, rounds=1, scores=True):
+    """Krum selections from (summed) krum_pair_sq sums: the exact route."""
+    n = int(A.shape[0])
+    order = torch.empty(rounds, dtype=torch.int32, device=A.device)
+    sc = torch.empty(n, dtype=torch.float32, device=A.device) if scores else None
+    nb = _lib.query_bytes("sra_krum_from_pairs_workspace_bytes", n)
+    ws = _workspace(nb, A.device)
+    _lib.call("sra_krum_from_pairs", A.contiguous().data_ptr(), n, int(f), int(rounds), order.data_ptr(),
+              sc.data_ptr() if sc is not None else None, ws.data_ptr(), nb, _stream_ptr(A.device))
+    return order, sc
+
+
 def gather_rows(X, rows, out=None):
     """out[r] = X[rows[r]] with `rows` a device int32 tensor (no host sync)."""
     X, n, d, ldx = as_matrix(X)

@@ -15,7 +15,12 @@ each rank reads only its N x d_r block:
   mean), so each rank computes the Gram of its block and one reduce of N*N
   fp64 (128 KiB at N=128) sums them on rank 0, which alone scores the N x N
   matrix (the score matrix stays on one GPU) and broadcasts the chosen
-  index(es); the chosen client's row is assembled with the same all-gather;
+  index(es); the chosen client's row is assembled with the same all-gather.
+  Where the unsharded engine takes its exact per-pair route (a NaN / inf
+  client, a squared distance beyond fp32's range, or d <= 1024), so does the
+  sharded one: ||a - b||^2 is a sum over column shards, so every rank forms
+  its class-coded pair sums and a second reduce sums them for the scoring
+  rank (``_krum_order``);
 * Bulyan's median / trimmed-mean selection rounds: one all-reduce of the
   <= N fp64 distance partials per round (the only per-round exchange), the
   pick made identically on every rank, then the local per-coordinate stage.
@@ -122,39 +127,81 @@ def coordinatewise(local_fn, X_shard, d, align=1, group=None):
     return gather_columns(local_fn(X_shard), d, align, group)
 
 
-def _gram_pick(G, pick, count, group=None):
-    """Sum the ranks' partial Grams on the group's first rank only, run
-    ``pick(G) -> (count,) int tensor`` there (the N x N scoring stays on one
-    GPU) and broadcast the indices; without a process group, pick(G)."""
-    if not dist.is_initialized():
-        return pick(G)
+# krum.hip kExactMaxD: layers this narrow always take the exact per-pair route
+EXACT_MAX_D = 1024
+
+
+def needs_exact(G, d):
+    """sra_krum_select_f32's switch to the exact per-pair route, evaluated on
+    the (summed) centred Gram: a narrow layer (d <= 1024), a non-finite
+    diagonal entry (a NaN / inf client; the centring spreads it over every
+    entry) or a squared distance G_ii + G_jj - 2 G_ij beyond fp32's range
+    (krum.hip krum_dist_kernel)."""
+    if d <= EXACT_MAX_D:
+        return True
+    dg = G.diagonal()
+    if not bool(torch.isfinite(dg).all()):
+        return True
+    sq = dg[:, None] + dg[None, :] - 2.0 * G
+    return bool((sq > 3.0e38).any())
+
+
+def _krum_order(G, X_shard, d, f, rounds, group=None, exact=None, bucket_size=1):
+    """The Krum selection order (``rounds`` picks) of a column-sharded layer,
+    on every rank.
+
+    The ranks' partial centred Grams ``G`` are summed on the group's first
+    rank, which decides the route as the unsharded engine does
+    (``needs_exact``) and broadcasts it.  Gram route: that rank scores the
+    summed Gram (``exact["krum_rounds"]``).  Exact route (robust_estimator.py:
+    242 computes every distance from the rows): every rank forms the class-
+    coded pair sums of its own columns (``exact["pair_sq"](X_shard,
+    bucket_size)``, sra_krum_pair_sq_f32 -- NaN / inf coded in place, so the
+    fp64 sum of the ranks' partials keeps the reference's NaN / inf classes),
+    a second reduce sums them on the first rank, which scores them
+    (``exact["krum_from_pairs"]``).  Either way the N x N scoring stays on one
+    GPU and one broadcast hands the order to every rank.  Without ``exact``
+    ops the Gram route is always taken."""
+    on = dist.is_initialized()
     _, rank = _world(group)
-    root = dist.get_global_rank(group, 0) if group is not None else 0
-    _reduce(G, root, group)
-    idx = torch.zeros(count, dtype=torch.int64, device=G.device)
-    if rank == 0:
-        idx.copy_(torch.as_tensor(pick(G), device=G.device).reshape(count).to(torch.int64))
-    _broadcast(idx, root, group)
+    root = (dist.get_global_rank(group, 0) if group is not None else 0) if on else 0
+    if on:
+        _reduce(G, root, group)
+    flag = torch.zeros(1, dtype=torch.int32, device=G.device)
+    if rank == 0 and exact is not None and "pair_sq" in exact:
+        flag.fill_(1 if needs_exact(G, d) else 0)
+    if on:
+        _broadcast(flag, root, group)
+    idx = torch.zeros(rounds, dtype=torch.int64, device=G.device)
+    if int(flag.item()):
+        A = exact["pair_sq"](X_shard, bucket_size).to(torch.float64).contiguous()
+        if on:
+            _reduce(A, root, group)
+        if rank == 0:
+            idx.copy_(torch.as_tensor(exact["krum_from_pairs"](A, f, rounds), device=G.device)
+                      .reshape(rounds).to(torch.int64))
+    elif rank == 0:
+        idx.copy_(torch.as_tensor(exact["krum_rounds"](G, f, rounds), device=G.device).reshape(rounds).to(torch.int64))
+    if on:
+        _broadcast(idx, root, group)
     return idx
 
 
-def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1):
+def krum(gram_fn, select_fn, X_shard, d, f, group=None, align=1, exact=None):
     """Krum over a column-sharded layer.
 
     gram_fn(X_shard) -> (N, N) float64 partial centred Gram;
     select_fn(G, f) -> index of the chosen client (from the full Gram).
-    Returns (full row of the chosen client, index).
-
-    Deviation from the single-GPU engine.krum: sra_krum_select_f32 re-derives
-    the distances of near-tied or non-finite pairs exactly from the rows (the
-    Gram's |a|^2 + |b|^2 - 2ab cancels there, and inf - inf is NaN); a
-    sharded layer's rows are split over the ranks, so the pick here always
-    comes from the summed Gram.  Finite, well-separated data pick the same
-    client (tests/test_gpu_shard2.py); ties within the Gram's rounding and
-    inf entries can pick differently than the reference."""
+    exact (optional): {"pair_sq", "krum_from_pairs"} -- the exact per-pair
+    route of ``_krum_order``, taken where sra_krum_select_f32 takes it
+    unsharded (NaN / inf clients, fp32-overflowing or d <= 1024), so the pick
+    equals the single-GPU engine's and the reference's there too.
+    Returns (full row of the chosen client, index)."""
     G = gram_fn(X_shard).to(torch.float64).contiguous()
+    ops = dict(exact or {})
+    ops["krum_rounds"] = lambda g, ff, rounds: torch.tensor([int(select_fn(g, ff))])
     # (a 1-rank group still goes through the collectives)
-    idx = int(_gram_pick(G, lambda g: torch.tensor([int(select_fn(g, f))]), 1, group)[0])
+    idx = int(_krum_order(G, X_shard, d, f, 1, group, ops)[0])
     row = gather_columns(X_shard[idx], d, align, group)
     return row, idx
 
@@ -171,7 +218,9 @@ def mom_krum(ops, X_shard, d, f, bucket_size=3, group=None, align=1):
     all-gathered.  Returns (full mean row of the chosen bucket, bucket index)."""
     n = int(X_shard.shape[0])
     G = ops["gram_buckets"](X_shard, bucket_size).to(torch.float64).contiguous()
-    idx = int(_gram_pick(G, lambda g: torch.tensor([int(ops["krum_select"](g, f))]), 1, group)[0])
+    kops = {k: ops[k] for k in ("pair_sq", "krum_from_pairs") if k in ops}
+    kops["krum_rounds"] = lambda g, ff, rounds: torch.tensor([int(ops["krum_select"](g, ff))])
+    idx = int(_krum_order(G, X_shard, d, f, 1, group, kops, bucket_size)[0])
     lo = idx * bucket_size
     part = ops["bucket_mean"](X_shard[lo:min(lo + bucket_size, n)])
     return gather_columns(part, d, align, group), idx
@@ -204,7 +253,7 @@ def bulyan(ops, X_shard, d, f, aggsubfunc="trimmedmean", group=None, align=1):
     on = dist.is_initialized()   # (a 1-rank group still goes through the collectives)
     if aggsubfunc == "krum":
         G = ops["gram"](X_shard).to(torch.float64).contiguous()
-        order = _gram_pick(G, lambda g: ops["krum_rounds"](g, int(f), theta), theta, group)
+        order = _krum_order(G, X_shard, d, int(f), theta, group, ops)
         S = X_shard.index_select(0, order.to(torch.long)).contiguous()
     else:
         if aggsubfunc not in ("median", "trimmedmean"):
@@ -333,6 +382,9 @@ def engine_ops():
         "gram_buckets": lambda X, bs: engine.gram_buckets(X, bs),
         "bucket_mean": lambda R: engine.bucket_means(R, int(R.shape[0]), 1)[0],
         "krum_select": select_fn,
+        # the exact per-pair route (_krum_order)
+        "pair_sq": lambda X, bs=1: engine.krum_pair_sq(X, bs),
+        "krum_from_pairs": lambda A, f, rounds: engine.krum_from_pairs(A, f, rounds, scores=False)[0],
         # (X_cols, out_view) forms for pipelined_coordinatewise
         "average_into": lambda X, o: engine.average(X, out=o),
         "median_into": lambda X, o: engine.median(X, out=o),

@@ -53,7 +53,7 @@ def test_sharded_krum_bit_exact(nccl_group):
     x = make_rows(100, 30_000, seed=32, byz=20)
     X = torch.from_numpy(x).cuda()
     ops = shard.engine_ops()
-    row, idx = shard.krum(ops["gram"], ops["krum_select"], X, 30_000, 20)
+    row, idx = shard.krum(ops["gram"], ops["krum_select"], X, 30_000, 20, exact=ops)
     want_row, order = engine.krum(X, 20)
     assert idx == int(order.cpu()[0])
     assert torch.equal(row, want_row)

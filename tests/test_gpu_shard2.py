@@ -57,6 +57,28 @@ def _data():
     return x, xc5
 
 
+EXACT_FIXTURES = ["krum_nan_client_n12_f2", "krum_inf_clients_n12_f2", "krum_nan_two_n12_f2",
+                  "krum_nan_client_n128_f20", "krum_nan_client_n300_f30", "mom_krum_nan_client_n30_f3",
+                  "bulyan_krum_nan_client_n24_f5"]
+
+
+def exact_fixtures():
+    from conftest import load_fixture
+    return {nm: load_fixture(os.path.join(HERE, "golden", nm + ".npz")) for nm in EXACT_FIXTURES}
+
+
+def wide_nonfinite():
+    """SH-sized layers (d = 40,960: not narrow) with a NaN client / +-inf
+    entries: the summed Gram's non-finite diagonal switches the route."""
+    x, _ = _data()
+    nan = x.copy()
+    nan[37, 20_000] = np.nan
+    inf = x.copy()
+    inf[5, 100] = np.inf
+    inf[90, 30_000] = -np.inf
+    return {"nan": nan, "inf": inf}
+
+
 def _rank(rank, port, results):
     for p in (ROOT, HERE):
         if p not in sys.path:
@@ -82,10 +104,19 @@ def _rank(rank, port, results):
         cols = shard.cyclic_blocks(d, WORLD, rank, block)
         Xc = torch.from_numpy(np.ascontiguousarray(np.concatenate([x[:, lo:hi] for lo, hi in cols], axis=1))).cuda()
         out["trimmedmean"] = shard.pipelined_coordinatewise(ops["trimmedmean_into"], Xc, d, block).cpu().numpy()
+        # an explicit communication stream and small blocks (40 rounds): each
+        # round's all-gather is ordered after its block's k-select by an event
+        # on comm, while the next block's k-select runs on the compute stream
+        comm = torch.cuda.Stream()
+        block = 512
+        cols = shard.cyclic_blocks(d, WORLD, rank, block)
+        Xc = torch.from_numpy(np.ascontiguousarray(np.concatenate([x[:, lo:hi] for lo, hi in cols], axis=1))).cuda()
+        out["trimmedmean_comm"] = shard.pipelined_coordinatewise(ops["trimmedmean_into"], Xc, d, block,
+                                                                comm_stream=comm).cpu().numpy()
         # contiguous 256-aligned shards for the Gram / Bulyan layers
         lo, hi = shard.shard_bounds(d, WORLD, rank, align=256)
         Xs = torch.from_numpy(np.ascontiguousarray(x[:, lo:hi])).cuda()
-        row, idx = shard.krum(ops["gram"], ops["krum_select"], Xs, d, f, align=256)
+        row, idx = shard.krum(ops["gram"], ops["krum_select"], Xs, d, f, align=256, exact=ops)
         out["krum_row"], out["krum_idx"] = row.cpu().numpy(), idx
         row, idx = shard.mom_krum(ops, Xs, d, f, align=256)
         out["mom_krum_row"], out["mom_krum_idx"] = row.cpu().numpy(), idx
@@ -98,7 +129,29 @@ def _rank(rank, port, results):
         cols = shard.cyclic_blocks(dt, WORLD, rank, fblock)
         Xf = torch.from_numpy(np.ascontiguousarray(np.concatenate([xc5[:, lo:hi] for lo, hi in cols], axis=1))).cuda()
         out["c5_block"] = fblock
-        out["c5"] = shard.pipelined_coordinatewise(bench.filter_into("mom_filterl2"), Xf, dt, fblock).cpu().numpy()
+        out["c5"] = shard.pipelined_coordinatewise(bench.filter_into("mom_filterl2"), Xf, dt, fblock,
+                                                   comm_stream=comm).cpu().numpy()
+        # the exact per-pair route over shards: the live-reference NaN / inf
+        # fixtures (narrow layers) and full-width layers with a NaN / inf client
+        for name, rec in exact_fixtures().items():
+            xe, fe = rec["x"], int(rec["params"]["f"])
+            de = xe.shape[1]
+            lo, hi = shard.shard_bounds(de, WORLD, rank)
+            Xe = torch.from_numpy(np.ascontiguousarray(xe[:, lo:hi])).cuda()
+            if rec["func"] == "krum":
+                row, idx = shard.krum(ops["gram"], ops["krum_select"], Xe, de, fe, exact=ops)
+                out["exact_" + name] = (row.cpu().numpy(), idx)
+            elif rec["func"] == "mom_krum":
+                row, idx = shard.mom_krum(ops, Xe, de, fe)
+                out["exact_" + name] = (row.cpu().numpy(), idx)
+            else:
+                out["exact_" + name] = (shard.bulyan(ops, Xe, de, fe, "krum").cpu().numpy(), -1)
+        for name, xe in wide_nonfinite().items():
+            lo, hi = shard.shard_bounds(d, WORLD, rank, align=256)
+            Xe = torch.from_numpy(np.ascontiguousarray(xe[:, lo:hi])).cuda()
+            _, idx = shard.krum(ops["gram"], ops["krum_select"], Xe, d, f, align=256, exact=ops)
+            _, midx = shard.mom_krum(ops, Xe, d, f, align=256)
+            out["wide_" + name] = (idx, midx, shard.bulyan(ops, Xe, d, f, "krum", align=256).cpu().numpy())
         torch.cuda.synchronize()
         results[rank] = out
     finally:
@@ -113,13 +166,20 @@ def two_rank_hip():
     results = mgr.dict()
     port = _free_port()
     procs = [ctx.Process(target=_rank, args=(r, port, results)) for r in range(WORLD)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=240)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0, "HIP shard rank failed (exit code %s)" % p.exitcode
+    try:
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=240)
+    finally:
+        # a rank that failed leaves its peer blocked in a gloo collective:
+        # end every rank still alive before judging the exit codes
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=30)
+    codes = [p.exitcode for p in procs]
+    assert all(c == 0 for c in codes), "HIP shard rank failed (exit codes %s)" % codes
     return dict(results)
 
 
@@ -132,12 +192,28 @@ def unsharded():
     X = torch.from_numpy(x).cuda()
     f = SH["f"]
     want = {"trimmedmean": engine.trimmed_mean(X, 0.1).cpu().numpy()}
+    want["trimmedmean_comm"] = want["trimmedmean"]
     row, order = engine.krum(X, f)
     want["krum_row"], want["krum_idx"] = row.cpu().numpy(), int(order.cpu()[0])
     row, order = engine.mom_krum(X, f)
     want["mom_krum_row"], want["mom_krum_idx"] = row.cpu().numpy(), int(order.cpu()[0])
     for mode in ("krum", "median", "trimmedmean"):
         want["bulyan_" + mode] = engine.bulyan(X, f, mode).cpu().numpy()
+    for name, rec in exact_fixtures().items():
+        Xe = torch.from_numpy(rec["x"]).cuda()
+        fe = int(rec["params"]["f"])
+        if rec["func"] == "krum":
+            row, order = engine.krum(Xe, fe)
+            want["exact_" + name] = (row.cpu().numpy(), int(order.cpu()[0]))
+        elif rec["func"] == "mom_krum":
+            row, order = engine.mom_krum(Xe, fe)
+            want["exact_" + name] = (row.cpu().numpy(), int(order.cpu()[0]))
+        else:
+            want["exact_" + name] = (engine.bulyan(Xe, fe, "krum").cpu().numpy(), -1)
+    for name, xe in wide_nonfinite().items():
+        Xe = torch.from_numpy(xe).cuda()
+        want["wide_" + name] = (int(engine.krum(Xe, f)[1].cpu()[0]), int(engine.mom_krum(Xe, f)[1].cpu()[0]),
+                                engine.bulyan(Xe, f, "krum").cpu().numpy())
     fa = bench.FILTER_ARGS
     Xf = torch.from_numpy(xc5).cuda()
     want["c5"] = engine.mom_filter_l2(Xf, fa["eps"], fa["sigma"], fa["expansion"], fa["itv"],
@@ -145,7 +221,7 @@ def unsharded():
     return want
 
 
-@pytest.mark.parametrize("key", ["trimmedmean", "krum_idx", "krum_row", "mom_krum_idx", "mom_krum_row",
+@pytest.mark.parametrize("key", ["trimmedmean", "trimmedmean_comm", "krum_idx", "krum_row", "mom_krum_idx", "mom_krum_row",
                                  "bulyan_krum", "bulyan_median", "bulyan_trimmedmean", "c5"])
 def test_two_ranks_equal_unsharded(two_rank_hip, unsharded, key):
     assert two_rank_hip[0]["c5_block"] > 0
@@ -156,3 +232,30 @@ def test_two_ranks_equal_unsharded(two_rank_hip, unsharded, key):
             assert got == want, "rank %d %s" % (r, key)
         else:
             np.testing.assert_array_equal(got, want, err_msg="rank %d %s" % (r, key))
+
+
+@pytest.mark.parametrize("name", EXACT_FIXTURES)
+def test_two_ranks_exact_route_fixtures(two_rank_hip, unsharded, name):
+    """Krum / mom_krum / Bulyan-Krum on the live-reference NaN / inf fixtures,
+    column-sharded over two ranks: the exact per-pair route over shards picks
+    the reference's client (fixture `index` / `out`) and the unsharded
+    engine's."""
+    from conftest import load_fixture
+    rec = load_fixture(os.path.join(HERE, "golden", name + ".npz"))
+    want_out, want_idx = unsharded["exact_" + name]
+    for r in range(WORLD):
+        got_out, got_idx = two_rank_hip[r]["exact_" + name]
+        assert got_idx == want_idx
+        if "index" in rec:
+            assert got_idx == int(rec["index"])
+        np.testing.assert_array_equal(got_out, want_out)
+        np.testing.assert_array_equal(got_out, rec["out"])
+
+
+@pytest.mark.parametrize("name", ["nan", "inf"])
+def test_two_ranks_exact_route_wide(two_rank_hip, unsharded, name):
+    want = unsharded["wide_" + name]
+    for r in range(WORLD):
+        got = two_rank_hip[r]["wide_" + name]
+        assert got[0] == want[0] and got[1] == want[1]
+        np.testing.assert_array_equal(got[2], want[2])

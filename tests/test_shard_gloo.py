@@ -91,6 +91,50 @@ def cpu_bulyan_ops():
 BULYAN_CASE = dict(n=30, d=257, f=5, seed=14, byz=5)
 
 
+def cpu_exact_ops():
+    """sra_krum_pair_sq_f32 / sra_krum_from_pairs restated with numpy: the
+    class-coded fp64 sums of squared fp32 differences, and Krum scored from
+    sqrt(fp32(sum)) (np.sort puts NaN last, np.argmin takes the first NaN)."""
+    from oracle import robust_np as orc
+
+    def pair_sq(X, bs=1):
+        x = X.numpy()
+        if bs > 1:
+            nb = -(-x.shape[0] // bs)
+            x = np.array(orc.bucket_means(list(x), bs, nb), dtype=np.float32)
+        with np.errstate(all="ignore"):
+            diff = (x[:, None, :] - x[None, :, :]).astype(np.float64)
+            a = (diff * diff).sum(axis=-1)
+        return torch.from_numpy(np.triu(a, 1))
+
+    def krum_from_pairs(A, f, rounds):
+        a = A.numpy()
+        a = a + a.T
+        with np.errstate(all="ignore"):
+            dd = np.sqrt(a.astype(np.float32))
+        alive, order = list(range(a.shape[0])), []
+        for _ in range(rounds):
+            sc = orc.krum_scores_from_dist(dd[np.ix_(alive, alive)], f)
+            order.append(alive.pop(int(np.argmin(sc))))
+        return torch.tensor(order, dtype=torch.int32)
+
+    return {"pair_sq": pair_sq, "krum_from_pairs": krum_from_pairs}
+
+
+def exact_cases():
+    """(x, d, f) inputs for which the unsharded engine takes the exact route."""
+    _setup_paths()
+    from synth import make_rows
+    nan = make_rows(24, 2000, seed=21, byz=4)
+    nan[7, 1500] = np.nan
+    inf = make_rows(24, 2000, seed=22, byz=4)
+    inf[3, 10] = np.inf
+    inf[9, 1900] = -np.inf
+    narrow = make_rows(24, 777, seed=23, byz=4)
+    narrow[12] = narrow[5] + np.float32(1e-7)      # a near tie the Gram cannot resolve
+    return {"nan": (nan, 2000, 4), "inf": (inf, 2000, 4), "narrow": (narrow, 777, 4)}
+
+
 def _worker(rank, world, port, results):
     _setup_paths()
     from srfl_amd import shard
@@ -182,6 +226,15 @@ def _worker(rank, world, port, results):
         Xb = torch.from_numpy(np.ascontiguousarray(xb[:, lo:hi]))
         for mode in ("krum", "median", "trimmedmean"):
             out["bulyan_" + mode] = shard.bulyan(cpu_bulyan_ops(), Xb, c["d"], c["f"], mode).numpy()
+        # Krum's exact per-pair route over shards (NaN / inf clients, a narrow
+        # layer): class-coded pair sums per shard, one reduce, scored once
+        xops = cpu_exact_ops()
+        for name, (xe, de, fe) in exact_cases().items():
+            lo, hi = shard.shard_bounds(de, world, rank)
+            Xe = torch.from_numpy(np.ascontiguousarray(xe[:, lo:hi]))
+            _, idx = shard.krum(lambda X: torch.from_numpy(_centred_gram(X.numpy())), select, Xe, de, fe,
+                                exact=xops)
+            out["exact_" + name] = idx
         results[rank] = out
     finally:
         dist.destroy_process_group()
@@ -193,11 +246,17 @@ def _run(world):
     results = mgr.dict()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, results)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=180)
-        assert p.exitcode == 0, "gloo worker failed"
+    try:
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=180)
+    finally:
+        for p in procs:          # a failed rank leaves its peers in a collective
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs), "gloo worker failed: %s" % [p.exitcode for p in procs]
     return dict(results)
 
 
@@ -308,6 +367,32 @@ def test_sharded_krum_equals_unsharded(two_rank_results):
     for r in (0, 1):
         assert two_rank_results[r]["krum_idx"] == idx
         np.testing.assert_array_equal(two_rank_results[r]["krum_row"], row)
+
+
+@pytest.mark.parametrize("case", ["nan", "inf", "narrow"])
+def test_sharded_krum_exact_route(case, two_rank_results, three_rank_results):
+    """A NaN client, +-inf clients and a narrow layer: the sharded Krum takes
+    the exact per-pair route (shard.needs_exact on the summed Gram) and picks
+    the reference's client with 2 and 3 column shards."""
+    _setup_paths()
+    from oracle import robust_np as orc
+    x, d, f = exact_cases()[case]
+    with np.errstate(all="ignore"):
+        _, idx = orc.krum(list(x), f)
+    for res in (two_rank_results, three_rank_results):
+        for r in res:
+            assert res[r]["exact_" + case] == idx
+
+
+def test_needs_exact_triggers():
+    _setup_paths()
+    from srfl_amd import shard
+    g = torch.eye(4, dtype=torch.float64)
+    assert shard.needs_exact(g, 1024) and not shard.needs_exact(g, 1025)
+    g[2, 2] = float("nan")
+    assert shard.needs_exact(g, 5000)
+    g = torch.eye(4, dtype=torch.float64) * 2e38
+    assert shard.needs_exact(g, 5000)
 
 
 def test_sharded_mom_krum_equals_unsharded(two_rank_results):
