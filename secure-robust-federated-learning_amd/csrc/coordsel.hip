@@ -26,6 +26,10 @@
 // strides beyond 32-bit lane offsets, fall back to an LDS bitonic tile.
 #include "sra_common.hpp"
 
+namespace sra {
+#include "net_fused.inc"
+}
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -213,17 +217,27 @@ __global__ void __launch_bounds__(BS) select_reg_kernel(const float* __restrict_
   if (t < rem) out[base + t] = res;
 }
 
-// Exact-N trimmed mean (default): NaN pre-pass (a NaN-propagating max3 over
-// the column; NaNs, if any, are counted and mapped to +inf, which sorts them
-// last like numpy), then a network of 4-byte VOP2 v_min_f32 / v_max_f32
-// compare-exchanges -- half the code bytes of the VOP3 minimum3/maximum3
-// pairs; 1.5-2 % faster at N = 128 (the kernel is VALU-issue bound: ~2.99k
-// VALU instructions per 64-coordinate tile at 4 cycles each).
+// Exact-N trimmed mean (N = 128 / 100: the default and config C1's client
+// count) and median: 4-blocks sorted with 3-input min / med3 / max whose
+// NaN-propagating maxima double as the NaN check (a column with a NaN --
+// wave-uniform, rare -- reloads, counts the NaNs and maps them to +inf, which
+// sorts them last like numpy), then the pruned odd-even merges as a fused
+// three-input program (tools/fuse_net.py -> net_fused.inc): a compare-exchange
+// pair whose output feeds one later compare-exchange is folded into it as
+// min3 / max3 / med3, 2,554 -> 1,888 VALU ops for the north-star network
+// (trimmed mean N = 128), 26 % fewer; the kernel was VALU-issue bound.
+template <int MODE, int NX, int BX>
+struct FusedFor;
+template <> struct FusedFor<kTrimmed, 128, 12> { using T = FusedTm128; };
+template <> struct FusedFor<kTrimmed, 100, 10> { using T = FusedTm100; };
+template <> struct FusedFor<kMedian, 128, 0> { using T = FusedMed128; };
+template <> struct FusedFor<kMedian, 100, 0> { using T = FusedMed100; };
+
 template <int MODE, int NX, int BX>
 __global__ void __launch_bounds__(256) select_plain_kernel(const float* __restrict__ X, int64_t d, int64_t ldx,
                                                           float* __restrict__ out) {
-  constexpr int P = ((NX + 15) / 16) * 16;
-  constexpr int P2 = next_pow2(P);
+  using Prog = typename FusedFor<MODE, NX, BX>::T;
+  constexpr int kSlots = Prog::kSlots > NX ? Prog::kSlots : NX;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * 256;
   const int64_t rem = d - base;
   const unsigned t = threadIdx.x;
@@ -234,7 +248,7 @@ __global__ void __launch_bounds__(256) select_plain_kernel(const float* __restri
   const uint32_t ahi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
   const uint64_t ldb = static_cast<uint64_t>(ldx) * 4;
   typedef const __attribute__((address_space(1))) float gfloat;
-  float v[P2];
+  float v[kSlots];
   auto load_column = [&]() {
     uint64_t rp = (static_cast<uint64_t>(ahi) << 32) | alo;
 #pragma unroll
@@ -246,24 +260,6 @@ __global__ void __launch_bounds__(256) select_plain_kernel(const float* __restri
     }
   };
   load_column();
-  constexpr int kMedLo = (NX - 1) / 2;
-  constexpr int kMedHi = NX / 2;
-  constexpr int kOutLo = MODE == kMedian ? kMedLo : BX;
-  constexpr int kOutHi = MODE == kMedian ? kMedHi + 1 : NX - BX;
-  auto finish = [&](int nan_cnt) -> float {
-    float r;
-    if constexpr (MODE == kMedian) {
-      r = (NX & 1) ? v[kMedLo] : (v[kMedLo] + v[kMedHi]) * 0.5f;
-      if (nan_cnt > 0) r = qnan();
-    } else {
-      float acc = 0.f;
-#pragma unroll
-      for (int p = BX; p < NX - BX; ++p) acc += v[p];
-      r = acc / static_cast<float>(NX - 2 * BX);
-      if (nan_cnt > BX) r = qnan();
-    }
-    return r;
-  };
   // rare slow path: count NaNs, map them to +inf (sorted last, like numpy)
   auto nan_map = [&]() -> int {
     int cnt = 0;
@@ -275,26 +271,27 @@ __global__ void __launch_bounds__(256) select_plain_kernel(const float* __restri
     }
     return cnt;
   };
+  // sorted 4-blocks whose NaN-propagating maxima double as the NaN check
+  const float m = sort4_blocks_nancheck<NX>(v);
+  int cnt = 0;
+  if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {   // rare: redo the blocks NaN-free
+    load_column();
+    cnt = nan_map();
+    sort4_blocks<NX>(v);
+  }
+  fused_network<Prog>(v);
   float res;
-  if constexpr (NX == 128) {   // (at N = 100 the extra live ranges cost a wave per SIMD)
-    // sorted 4-blocks whose NaN-propagating maxima double as the NaN check
-    const float m = sort4_blocks_nancheck<NX>(v);
-    int cnt = 0;
-    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) {   // rare: redo the blocks NaN-free
-      load_column();
-      cnt = nan_map();
-      sort4_blocks<NX>(v);
-    }
-    network_plain<P2, NX, kOutLo, kOutHi, kNetFrom4>(v);
-    res = finish(cnt);
+  if constexpr (MODE == kMedian) {
+    res = (NX & 1) ? v[Prog::kOut[0]] : (v[Prog::kOut[0]] + v[Prog::kOut[1]]) * 0.5f;
+    if (cnt > 0) res = qnan();
   } else {
-    float m = v[0];
+    // sequential ascending-order fp32 sum of the kept ranks (numpy's axis-0
+    // reduce, which starts from the identity +0), then the division
+    float acc = 0.f;
 #pragma unroll
-    for (int i = 1; i < NX; ++i) m = __builtin_elementwise_maximum(m, v[i]);
-    int cnt = 0;
-    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(m)) != 0) cnt = nan_map();
-    network_plain<P2, NX, kOutLo, kOutHi, kNetSort>(v);
-    res = finish(cnt);
+    for (int p = 0; p < Prog::kOuts; ++p) acc += v[Prog::kOut[p]];
+    res = acc / static_cast<float>(NX - 2 * BX);
+    if (cnt > BX) res = qnan();   // a NaN sits in the kept window
   }
   if (t < rem) out[base + t] = res;
 }
@@ -423,19 +420,21 @@ __global__ void __launch_bounds__(256) select_quad_kernel(const float* __restric
   const uint32_t sgn0 = (L == 2 ? (h == 1) : (h == 1 || h == 2)) ? 0x80000000u : 0u;
   const uint32_t odd = (h & 1) ? 0x80000000u : 0u;
   flip(v, sgn0);
+  // in-lane sort and half-cleaner cascades as fused three-input programs
+  // (tools/fuse_net.py: 2,622 -> 1,940 and 896 -> 704 VALU ops)
   sort4_blocks<128>(v);
-  network_plain<128, 128, 0, 128, kNetFrom4>(v);
+  fused_sort128<FusedSort128>(v);
   // level 1: pairs (h, h^1)
   cross_step<1>(v);
   flip(v, odd);
-  network_plain<128, 128, 0, 128, kNetMerge>(v);
+  fused_sort128<FusedBitonic128>(v);
   if constexpr (L == 4) {
     // level 2: stride-256 step with h^2, stride-128 step with h^1 (odd lanes flipped around it)
     cross_step<2>(v);
     flip(v, odd);
     cross_step<1>(v);
     flip(v, odd);
-    network_plain<128, 128, 0, 128, kNetMerge>(v);
+    fused_sort128<FusedBitonic128>(v);
   }
   // total NaN count of the coordinate
   if constexpr (L == 2) {
@@ -560,18 +559,24 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
   const bool trim128 = MODE == kTrimmed && n == 128 && lo == 12 && hi == 116;
   const bool trim100 = MODE == kTrimmed && n == 100 && lo == 10 && hi == 90;
 
-  // Exact-N trimmed mean: the VOP2 min/max network with a NaN pre-pass
-  // (measured 1.5-2 % faster than the VOP3 NaN-propagating one at N = 128,
-  // d = 1e8).  The median keeps the NaN-propagating network (no pre-pass,
-  // fewer VALU ops).
-  if constexpr (MODE == kTrimmed) {
+  // Exact N = 128 / 100 (trimmed mean at beta = 0.1, median): the fused
+  // three-input networks behind a NaN check (select_plain_kernel).
+  if constexpr (MODE == kTrimmed || MODE == kMedian) {
     const int64_t blocks = cdiv(d, 256);
     if (trim128) {
-      hipLaunchKernelGGL((select_plain_kernel<MODE, 128, 12>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
+      hipLaunchKernelGGL((select_plain_kernel<kTrimmed, 128, 12>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
       return launch_status("select_plain_kernel");
     }
     if (trim100) {
-      hipLaunchKernelGGL((select_plain_kernel<MODE, 100, 10>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
+      hipLaunchKernelGGL((select_plain_kernel<kTrimmed, 100, 10>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
+      return launch_status("select_plain_kernel");
+    }
+    if (MODE == kMedian && n == 128) {
+      hipLaunchKernelGGL((select_plain_kernel<kMedian, 128, 0>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
+      return launch_status("select_plain_kernel");
+    }
+    if (MODE == kMedian && n == 100) {
+      hipLaunchKernelGGL((select_plain_kernel<kMedian, 100, 0>), dim3(blocks), dim3(256), 0, s, X, d, ldx, out);
       return launch_status("select_plain_kernel");
     }
   }
@@ -582,10 +587,6 @@ static int launch_select(const float* X, int n, int64_t d, int64_t ldx, int lo, 
                        d, ldx, lo, hi, out);                                                                     \
     return launch_status("select_reg_kernel");                                                                   \
   } while (0)
-    if (trim128) SRA_SEL1(128, 128, 12);
-    if (trim100) SRA_SEL1(112, 100, 10);
-    if (MODE == kMedian && n == 128) SRA_SEL1(128, 128, -1);
-    if (MODE == kMedian && n == 100) SRA_SEL1(112, 100, -1);
     switch (P) {
       case 16: SRA_SEL1(16, 0, -1);
       case 32: SRA_SEL1(32, 0, -1);

@@ -413,32 +413,80 @@ __device__ __forceinline__ void bitonic_merge(float (&v)[P2]) {
   if constexpr (P2 > 1) net_run<Plan>(v, std::make_index_sequence<Plan::value.n>{});
 }
 
-// Plain (NaN-free) variants: lo = v_min_f32, hi = v_max_f32.  Used after NaNs
-// have been mapped to +inf (their count is tracked separately).
+// Plain (NaN-free) variants, used after NaNs have been mapped to +inf (their
+// count is tracked separately).  CE form CEF:
+//   0: lo = v_min_f32, hi = v_max_f32 (4-byte VOP2 each);
+//   1: hi recovered as a ^ b ^ lo with one v_bitop3_b32 (truth table 0x96 =
+//      xor3): v_min_f32 of two non-NaN values returns one of its operands bit
+//      for bit (fp32 denormals are preserved in these kernels, +-0 are both
+//      operands), so the xor of all three is exactly the other one;
+// Form 1 is 1.5-3.5 % faster than form 0 on register-resident columns
+// (tools/ubench/net_rate.hip) but 3 % SLOWER in select_plain_kernel, whose
+// clock is power-limited by the HBM stream beside the VALU (three register
+// reads per xor3 against two per max): the product uses form 0.
+template <int CEF>
 __device__ __forceinline__ void ce_pair_plain(float& a, float& b) {
   float lo;
-  asm("v_min_f32 %0, %2, %1\n\tv_max_f32 %1, %2, %1" : "=&v"(lo), "+v"(b) : "v"(a));
+  if constexpr (CEF == 0)
+    asm("v_min_f32 %0, %2, %1\n\tv_max_f32 %1, %2, %1" : "=&v"(lo), "+v"(b) : "v"(a));
+  else
+    asm("v_min_f32 %0, %2, %1\n\tv_bitop3_b32 %1, %2, %1, %0 bitop3:0x96" : "=&v"(lo), "+v"(b) : "v"(a));
   a = lo;
 }
 
-template <typename Plan, int Q, int P2>
+template <typename Plan, int Q, int P2, int CEF>
 __device__ __forceinline__ void net_op_plain(float (&v)[P2]) {
   constexpr int kd = Plan::value.kind[Q], x = Plan::value.a[Q], y = Plan::value.b[Q];
-  if constexpr (kd == kOpCE) ce_pair_plain(v[x], v[y]);
+  if constexpr (kd == kOpCE) ce_pair_plain<CEF>(v[x], v[y]);
   else if constexpr (kd == kOpMin) v[x] = __builtin_fminf(v[x], v[y]);
   else if constexpr (kd == kOpMax) v[y] = __builtin_fmaxf(v[x], v[y]);
   else v[x] = v[y];
 }
 
-template <typename Plan, int P2, size_t... Q>
+template <typename Plan, int P2, int CEF, size_t... Q>
 __device__ __forceinline__ void net_run_plain(float (&v)[P2], std::index_sequence<Q...>) {
-  (net_op_plain<Plan, Q>(v), ...);
+  (net_op_plain<Plan, Q, P2, CEF>(v), ...);
 }
 
-template <int P2, int PR, int OLO, int OHI, int KIND>
+template <int P2, int PR, int OLO, int OHI, int KIND, int CEF = 0>
 __device__ __forceinline__ void network_plain(float (&v)[P2]) {
   using Plan = NetPlan<P2, PR, OLO, OHI, KIND>;
-  if constexpr (P2 > 1) net_run_plain<Plan>(v, std::make_index_sequence<Plan::value.n>{});
+  if constexpr (P2 > 1) net_run_plain<Plan, P2, CEF>(v, std::make_index_sequence<Plan::value.n>{});
+}
+
+// ---------------------------------------------------------------------------
+// Straight-line three-input networks (tools/fuse_net.py -> csrc/net_fused_*.inc).
+// A merge network's compare-exchange pair whose one output feeds a single
+// later compare-exchange is folded into that consumer as min3 / max3 / med3 of
+// the pair's inputs (valid where the 0-1 principle says so), e.g. for the
+// north-star network 2,554 -> 1,888 VALU ops.  Prog::k* are the constexpr
+// tables (kind, dst, a, b, c) over register slots v[0 .. Prog::kSlots) (the
+// CPU tests re-run them), Prog::run the same program as code; NaN-free inputs
+// (callers map NaN to +inf first).
+// ---------------------------------------------------------------------------
+// Prog::run is the program as inline asm, a few ops per statement: with
+// builtins the compiler re-splits min3 / max3 into shared two-input mins,
+// canonicalises med3 operands and hoists for ILP (259 registers at N = 128:
+// one wave per SIMD); asm keeps the generator's order and its bounded live
+// set (221), and grouping cuts the hazard s_nops the compiler puts after
+// dependent asm boundaries.
+template <class Prog, int S>
+__device__ __forceinline__ void fused_network(float (&v)[S]) {
+  Prog::run(v);
+}
+
+// In-place form for a full sort of v[0 .. 128): the program runs on a
+// kSlots-wide copy and the ranks are read back in order (register renaming,
+// no moves unless the allocator needs them).
+template <class Prog>
+__device__ __forceinline__ void fused_sort128(float (&v)[128]) {
+  static_assert(Prog::kOuts == 128, "a full 128-value program");
+  float w[Prog::kSlots > 128 ? Prog::kSlots : 128];
+#pragma unroll
+  for (int i = 0; i < 128; ++i) w[i] = v[i];
+  fused_network<Prog>(w);
+#pragma unroll
+  for (int i = 0; i < 128; ++i) v[i] = w[Prog::kOut[i]];
 }
 
 // Sort the aligned blocks of 4 of v[0..PR) (NaN-free) with 7 VALU ops each

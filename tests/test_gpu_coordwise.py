@@ -150,3 +150,45 @@ def test_multilane_path_bitexact(n):
         np.testing.assert_array_equal(engine.median(X).cpu().numpy(), orc.median(list(x)))
         for beta in (0.0, 0.3):
             np.testing.assert_array_equal(engine.trimmed_mean(X, beta).cpu().numpy(), orc.trimmed_mean(list(x), beta))
+
+
+@pytest.mark.parametrize("n", [100, 128, 129, 256, 512])
+def test_denormals_and_signed_zeros_bitwise(n):
+    """The plain networks recover each compare-exchange's max as a ^ b ^ min
+    (csrc/sra_common.hpp ce_pair_plain), which is exact only if v_min_f32
+    returns one of its operands bit for bit: columns of fp32 denormals of
+    both signs, ±0, ±FLT_MAX and ±inf must come out as the oracle's bit
+    patterns (compared as uint32, so -0 != +0), for the exact-N kernel
+    (N = 100 / 128) and the multi-lane one (N > 128)."""
+    rng = np.random.default_rng(77 + n)
+    d = 2048 + 17
+    x = make_rows(n, d, seed=n)
+    tiny = np.float32(1.4e-45)
+    pool = np.array([0.0, -0.0, tiny, -tiny, 3 * tiny, -7 * tiny, np.float32(1.1754942e-38),
+                     -np.float32(1.1754942e-38), np.finfo(np.float32).max, -np.finfo(np.float32).max,
+                     np.inf, -np.inf], np.float32)
+    # a third of the columns entirely from the special pool, the rest salted
+    cols = rng.choice(d, d // 3, replace=False)
+    x[:, cols] = rng.choice(pool, size=(n, cols.size))
+    x[rng.integers(0, n, 4000), rng.integers(0, d, 4000)] = rng.choice(pool, 4000)
+    # all-negative-zero window columns (the sum starts from the first kept row)
+    x[:, :3] = np.float32(-0.0)
+    X = torch.from_numpy(x).cuda()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want_tm = np.asarray(orc.trimmed_mean(list(x)), np.float32)
+        want_md = np.asarray(orc.median(list(x)), np.float32)
+    got_tm = engine.trimmed_mean(X).cpu().numpy()
+    got_md = engine.median(X).cpu().numpy()
+    np.testing.assert_array_equal(got_tm, want_tm)
+    np.testing.assert_array_equal(got_md, want_md)
+    # bit patterns, except where the sorted kept window mixes -0 and +0 (numpy's
+    # tie order among equal zeros is its sort's, not a defined one)
+    srt = np.sort(x, axis=0)
+    b = int(n * 0.1)
+    win = srt[b:n - b]
+    mixed = (np.signbit(win) & (win == 0)).any(axis=0) & (~np.signbit(win) & (win == 0)).any(axis=0)
+    ok = ~mixed
+    assert ok[:3].all()
+    np.testing.assert_array_equal(got_tm.view(np.uint32)[ok], want_tm.view(np.uint32)[ok])

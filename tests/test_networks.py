@@ -91,3 +91,83 @@ def test_sort4_block():
         assert sort4(*perm) == sorted(perm)
     for bits in itertools.product([0, 1, 2], repeat=4):   # ties included
         assert sort4(*bits) == sorted(bits)
+
+
+# ---------------------------------------------------------------------------
+# the fused three-input programs (csrc/net_fused.inc, tools/fuse_net.py)
+# ---------------------------------------------------------------------------
+INC = os.path.join(os.path.dirname(HDR), "net_fused.inc")
+
+
+def fused_programs():
+    """Parse the generated header: {name: (kind, dst, a, b, c, out, slots)}."""
+    text = open(INC).read()
+    progs = {}
+    for m in re.finditer(r"struct (\w+) \{(.*?)\n\};", text, flags=re.S):
+        body = m.group(2)
+
+        def arr(nm):
+            blk = re.search(r"%s\[\d+\] = \{([^}]*)\}" % nm, body).group(1)
+            return [int(t) for t in blk.replace("\n", " ").split(",") if t.strip()]
+        slots = int(re.search(r"kSlots = (\d+)", body).group(1))
+        progs[m.group(1)] = (arr("kKind"), arr("kDst"), arr("kA"), arr("kB"), arr("kC"), arr("kOut"), slots)
+    return progs
+
+
+def run_fused(prog, X):
+    kind, dst, A, B, C, out, slots = prog
+    v = [None] * slots
+    for i in range(X.shape[0]):
+        v[i] = X[i]
+    for k, d, a, b, c in zip(kind, dst, A, B, C):
+        if k == 1:
+            r = np.minimum(v[a], v[b])
+        elif k == 2:
+            r = np.maximum(v[a], v[b])
+        elif k == 3:
+            r = np.minimum(np.minimum(v[a], v[b]), v[c])
+        elif k == 4:
+            r = np.maximum(np.maximum(v[a], v[b]), v[c])
+        else:
+            assert k == 5
+            r = np.maximum(np.minimum(v[a], v[b]), np.minimum(np.maximum(v[a], v[b]), v[c]))
+        v[d] = r
+    return np.array([v[o] for o in out])
+
+
+def test_fused_programs_sort():
+    """Every generated program, as the kernels run it, returns np.sort's kept
+    ranks on columns with heavy ties (integers in [-3, 3]) and on Gaussian
+    columns, in its input form (sorted 4-blocks + +inf pads, or bitonic)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HDR)), "..", "tools"))
+    import fuse_net as fn
+    progs = fused_programs()
+    assert set(progs) == {p[0] for p in fn.PROGRAMS}
+    for name, p2, pr, olo, ohi, net in fn.PROGRAMS:
+        for seed in (3, 4):
+            X, want = fn.random_inputs(p2, pr, net, 4000, seed)
+            got = run_fused(progs[name], X)
+            np.testing.assert_array_equal(got, want[olo:ohi], err_msg=name)
+        rng = np.random.default_rng(5)
+        T = rng.integers(-3, 4, size=(pr, 4000)).astype(np.float64)
+        want = np.sort(T, axis=0)
+        if net == "from4":
+            for b in range(0, pr, 4):
+                T[b:b + 4] = np.sort(T[b:b + 4], axis=0)
+        else:
+            T = np.vstack([np.sort(T[:pr // 2], axis=0), np.sort(T[pr // 2:], axis=0)[::-1]])
+        T = np.vstack([T, np.full((p2 - pr, 4000), np.inf)])
+        np.testing.assert_array_equal(run_fused(progs[name], T), want[olo:ohi], err_msg=name)
+
+
+def test_fused_header_is_generated():
+    """net_fused.inc is exactly what tools/fuse_net.py emits today."""
+    import subprocess
+    import sys
+    import tempfile
+    tool = os.path.join(os.path.dirname(os.path.dirname(HDR)), "..", "tools", "fuse_net.py")
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "net_fused.inc")
+        subprocess.run([sys.executable, tool, "--emit-all", out], check=True, capture_output=True)
+        assert open(out).read() == open(INC).read()
