@@ -310,8 +310,11 @@ int sra_mom_filter_workspace_bytes(int64_t nbuckets, int64_t d, int32_t itv, siz
  * holds the n clients; filtered row r is the np.mean of clients
  * [r * bucket_size, min((r + 1) * bucket_size, n)), formed inside the chunk-Gram
  * loads (a sequential fp32 sum over the bucket's clients / their count, the
- * bits sra_bucket_mean_f32 writes) -- the bucket matrix is never written as a
- * whole; each batch's bucket rows go to the workspace for the chunk means.
+ * bits sra_bucket_mean_f32 writes) -- no separate bucket-mean pass, but each
+ * batch's bucket rows (nbuckets x min(chunks, 16384) x itv floats) are written
+ * once to the workspace for the chunk means: up to d = 1.6e7 at itv 1000 that
+ * is the whole bucket matrix (6.4 GB at C5), which
+ * sra_mom_filter_workspace_bytes reports.
  * Results equal sra_bucket_mean_f32 followed by sra_filter_f32 bit for bit.
  * nbuckets <= 128 (SRA_ERR_UNSUPPORTED above: run the two calls instead); an
  * empty trailing bucket -> SRA_ERR_EMPTY_BUCKET (the reference's ValueError). */

@@ -1,5 +1,5 @@
 #!/bin/bash
-# On the GPU box, after tools/profile_round.sh (TAG) / tools/gpu_pmcw.sh / gpu_r4.sh pmc steps:
+# On the GPU box, after tools/profile_round.sh (TAG) / tools/gpu_pmcw.sh pmc steps:
 # fold the PMC CSVs into profiles/traffic.json + summaries, copy what is to be
 # kept to gpurun_out/keep/, and delete the per-dispatch CSVs (gpurun_out/ must
 # stay under 64 MiB to come back).  usage: bash tools/gpu_pmc_pack.sh TAG [pmc_dir ...]
