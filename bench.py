@@ -211,7 +211,7 @@ KERNEL_NAME = {
     "dba_median": "select_reg_kernel<128, kOrder> (lower median, DBA Helper.median)",
     "dba_weighted_sum": "rows_vec4_kernel<true> (DBA weighted_average_oracle)",
     "trimmedmean": "select_plain_kernel<1, 128, 12>",
-    "median": "select_reg_kernel<128, 0, 128>",
+    "median": "select_plain_kernel<0, 128, 0>",
     "average": "average_vec4_kernel",
     "krum": "whole krum op (bf16x3 gram_glds_kernel dominant; per-kernel split in profiles/)",
     "mom_krum": "whole mom_krum op (gram_bucket_kernel: bucket means fused into the bf16x3 Gram + scoring)",
@@ -238,7 +238,7 @@ def kernel_label(agg, n):
     if agg == "trimmedmean" and n == 100:
         return "select_plain_kernel<1, 100, 10>"
     if agg == "median" and n == 100:
-        return "select_reg_kernel<112, 0, 100>"
+        return "select_plain_kernel<0, 100, 0>"
     return KERNEL_NAME[agg]
 
 

@@ -59,3 +59,28 @@ def test_dba_module_needs_a_gpu():
     h = dba.HelperAggregation({"eta": 1})
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         h.median(None, {0: (10, {"w": torch.from_numpy(np.zeros(3, np.float32))})})
+
+
+def test_capi_validation_under_asan():
+    """The host side of every C-ABI entry point (argument validation,
+    workspace sizing, launch set-up) under AddressSanitizer: `make asan`
+    builds libsra_asan.so with -fsanitize=address on the host code only
+    (device code as usual), and tests/capi_asan_driver.py calls each symbol
+    of include/sra.h with null / zero / negative / huge / plausible arguments
+    in a subprocess with the ASan runtime preloaded.  Any overflow aborts it."""
+    import glob
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "secure-robust-federated-learning_amd", "csrc")
+    rt = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    if not rt:
+        pytest.skip("no clang ASan runtime in this image")
+    subprocess.run(["make", "-C", csrc, "-j8", "asan"], check=True, capture_output=True)
+    env = dict(os.environ, LD_PRELOAD=rt[-1], ASAN_OPTIONS="detect_leaks=0",
+               SRA_LIB=os.path.join(root, "build", "sra_asan", "libsra_asan.so"))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "capi_asan_driver.py")], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "asan driver:" in r.stdout and "AddressSanitizer" not in r.stderr

@@ -19,8 +19,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"trimmedmean": "select_plain_kernel", "median": "select_reg_kernel", "average": "average",
-            "trimmedmean_n100": "select_plain_kernel", "median_n100": "select_reg_kernel",
+DOMINANT = {"trimmedmean": "select_plain_kernel", "median": "select_plain_kernel", "average": "average",
+            "trimmedmean_n100": "select_plain_kernel", "median_n100": "select_plain_kernel",
             "trimmedmean_n512": "select_quad_kernel", "median_n512": "select_quad_kernel",
             "krum": "gram_glds_kernel", "dba_median": "select_reg_kernel", "dba_weighted_sum": "rows_vec4_kernel"}
 # Whole-op workloads (bench.py prices the whole call): traffic = the sum over
