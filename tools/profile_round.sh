@@ -29,7 +29,7 @@ filterl2|--agg filterl2 --d 1e7
 ex_noregret|--agg ex_noregret --d 1e7
 mom_filterl2|--agg mom_filterl2 --clients 512 --d 1.25e7
 mom_ex_noregret|--agg mom_ex_noregret --clients 512 --d 1.25e7"}
-PMC_WORKLOADS=${PMC_WORKLOADS:-"trimmedmean median average trimmedmean_n100 trimmedmean_n512 median_n512 krum"}
+PMC_WORKLOADS=${PMC_WORKLOADS:-"trimmedmean median average trimmedmean_n100 trimmedmean_n512 median_n512 krum bulyanmedian bulyantrimmedmean"}
 while IFS='|' read -r name args; do
   [[ -z "$name" ]] && continue
   [ -n "${SKIP_TRACE:-}" ] && continue
@@ -39,6 +39,8 @@ while IFS='|' read -r name args; do
   steps=$(printf '%s\n' "$args" | sed -n 's/.*--steps \([0-9]*\).*/\1/p')
   tr=$(find "$OUTD/$name" -name '*kernel_trace.csv' | head -1)
   [ -n "$tr" ] && python3 "$ROOT/tools/steady_stats.py" "$tr" "${steps:-20}" > "$OUTD/$name.steady.txt"
+  # keep the summaries only (gpurun copies back at most 64 MiB)
+  find "$OUTD/$name" -type f ! -name '*kernel_stats.csv' -delete
   echo "trace $name ok"
 done <<< "$WORKLOADS"
 for name in $PMC_WORKLOADS; do
@@ -47,6 +49,11 @@ for name in $PMC_WORKLOADS; do
     timeout -k 10 400 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d "$OUTD/pmc_${name}_$ctr" -o run \
       -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-host $args > "$OUTD/pmc_${name}_$ctr.log" 2>&1 \
       || { echo "pmc $name $ctr failed rc=$?"; exit 1; }
+    # the counter rows of this library's kernels only
+    for f in $(find "$OUTD/pmc_${name}_$ctr" -name '*counter_collection.csv'); do
+      python3 -c "import csv,sys; r=list(csv.reader(open(sys.argv[1]))); k=r[0].index('Kernel_Name'); w=csv.writer(open(sys.argv[1],'w',newline='')); w.writerow(r[0]); [w.writerow(x) for x in r[1:] if 'sra::' in x[k]]" "$f"
+    done
+    find "$OUTD/pmc_${name}_$ctr" -type f ! -name '*counter_collection.csv' -delete
     echo "pmc $name $ctr ok"
   done
 done
