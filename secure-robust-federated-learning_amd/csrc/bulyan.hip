@@ -28,6 +28,7 @@
 //   a NaN is among the kept values.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "sra_common.hpp"
 
@@ -63,28 +64,39 @@ __device__ __forceinline__ float ld_lane(const char* row, unsigned off) {
 // One round of the median / trimmed-mean modes as ONE pass over the remaining
 // rows (robust_estimator.py:297-322).  Per 256-coordinate block tile:
 //   1. each wave loads the column of every listed row (one lane per
-//      coordinate, the row list in VGPRs, row bases broadcast by readlane) and
-//      runs the k-select network -> the round's aggregate for its 64
+//      coordinate; row bases formed per tile as one 64-bit pointer per lane
+//      and broadcast by two readlanes, fetched two rows ahead of their load)
+//      and runs the k-select network -> the round's aggregate for its 64
 //      coordinates (written out: it is the t-th selected vector);
-//   2. it then re-issues the SAME loads, row by row (the lines it has just
-//      read: L2 / Infinity Cache hits, not HBM), writes agg - x to an LDS tile
-//      of 32 rows x 64 coordinates, and reads it back transposed -- lanes
-//      l and l + 32 hold row l's two 32-coordinate halves -- so each row's
+//   2. the listed rows' columns go, 32 rows at a time, into an LDS tile (from
+//      the step-1 copy in LDS or registers, or re-read: L2 / Infinity Cache
+//      lines, all re-reads issued at once), read back transposed -- lanes l
+//      and l + 32 hold row l's two 32-coordinate halves -- and each row's
 //      squared distance over the wave's 64 coordinates is an in-order fp32
-//      fma chain per half plus one cross-half add;
+//      fma chain of (agg - x)^2 per half plus one cross-half add;
 //   3. the block's four waves are added in order (fp32), into a per-block,
 //      per-row partial; bulyan_dist_reduce_kernel sums the blocks in order in
 //      fp64.  Deterministic for a given d (sharded or not: a shard's dist is
 //      its own columns' share).
 // Blocks take runs of consecutive tiles (one tile each up to d = 16.7M), so
 // the partial table is at most kRoundMaxBlocks x n floats.
-// Measured at N=128, f=20, d=1e7 (C3): 2.06 ms per P=128 round against 1.30 +
-// 0.58 ms for round 1's k-select and distance kernels; the re-read is served
-// by the Infinity Cache but still costs fabric bandwidth.
+// Round 6 (C3, N = 128, f = 20, d = 1e7; profiles/r06_bulyan_rounds_ab.txt):
+// per-round kernel 1.82 -> 1.45 ms at P = 128 (trimmed mean), 1.53 -> 1.40
+// (median).  PMC before the change: VALU ~55-60 % busy, as many scalar
+// instructions as vector ones (the per-row index, clamp and 64-bit multiply,
+// twice), and four cache-latency waits per tile in step 2.
 constexpr int kRoundMaxBlocks = 65536;
 
-template <int P, int MODE, bool COPY = false>  // MODE: 0 median, 1 trimmed; n in (P-16, P] (P=16: 1..16)
-__global__ void __launch_bounds__(256, (COPY && P > 64) ? 2 : 3) select_dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
+// Where step 2 takes each listed row's column from (template KL, KU):
+//   rows [0, KL)   copied into this wave's LDS tile in step 1 (KL = 0 or >= 32);
+//   rows [KL, KU)  kept in VGPRs across the network;
+//   rows [KU, P)   re-read (L2 / Infinity Cache).
+// Step 2 stages every row that is not already in LDS at tile row r % 32 (the
+// first 32 rows' slots, consumed by then), then reads the tile transposed and
+// forms res - x there: the same fp32 operations in the same order whatever
+// the split, so the distances do not depend on it.  W: waves per SIMD.
+template <int P, int MODE, int KL, int KU, int W>  // MODE: 0 median, 1 trimmed; n in (P-16, P] (P=16: 1..16)
+__global__ void __launch_bounds__(256, W) select_dist_rows_kernel(const float* __restrict__ X, int64_t ldx,
                                                                const int* __restrict__ rows, int nrows_x, int n_arg,
                                                                int64_t d,
                                                                int lo, int hi, int nan_all, float* __restrict__ out,
@@ -95,14 +107,18 @@ __global__ void __launch_bounds__(256, (COPY && P > 64) ? 2 : 3) select_dist_row
   const unsigned w = t >> 6;
   // the row list in VGPRs (lane l holds rows[l], rows[64 + l], ...): each
   // row index is then a readlane, not a dependent scalar load per row
+  // -- as 64-bit byte offsets (row * ldx * 4, the row checked and clamped
+  // once here): a row's base is then two readlanes and one 64-bit scalar add
+  // per tile (the index, clamp and multiply per row and pass were ~12 scalar
+  // instructions and a branch each, as many as the network's VALU work)
+  // (formed per tile from the list: nothing but the list pointer stays live
+  // across tiles, which the 256-VGPR copy variants need)
   constexpr int RW = (P + 63) / 64;
-  int rl[RW];
-#pragma unroll
-  for (int q = 0; q < RW; ++q) {
-    const int li = 64 * q + static_cast<int>(lane);
-    rl[q] = rows[li < n_arg ? li : n_arg - 1];
-  }
-  __shared__ float dl[4][32][68];   // row stride 68 words: the transposed b128 reads spread over the banks
+  static_assert(KL == 0 || (KL >= 32 && KL <= P), "LDS copy rows");
+  static_assert(KU == 0 || (KU >= KL && KU <= P), "register copy rows");
+  constexpr int KR = KL > 32 ? KL : 32;
+  __shared__ float dl[4][KR][68];   // row stride 68 words: the transposed b128 reads spread over the banks
+  __shared__ float rsl[4][64];      // the round's aggregate of each wave's 64 coordinates
   __shared__ float wsum[4][P];
   float bs = 0.f;
   const int n_out = n_arg;
@@ -114,48 +130,88 @@ __global__ void __launch_bounds__(256, (COPY && P > 64) ? 2 : 3) select_dist_row
     const int64_t rem = d - base;
     const unsigned last = rem < 256 ? static_cast<unsigned>(rem - 1) : 255u;
     const unsigned off = (t < last ? t : last) * 4u;
-    // per tile: otherwise the row bases are hoisted out of the tile loop and
-    // held (spilled) in SGPRs
+    // this tile's row bases, one per lane (per tile: hoisted out of the tile
+    // loop they would be held, spilled, across it)
+    const uint64_t xa = reinterpret_cast<uint64_t>(X + base);
+    uint32_t plo[RW], phi[RW];
 #pragma unroll
-    for (int q = 0; q < RW; ++q) asm volatile("" : "+v"(rl[q]));
+    for (int q = 0; q < RW; ++q) {
+      const int li = 64 * q + static_cast<int>(lane);
+      const int row = checked_row(rows[li < n_arg ? li : n_arg - 1], nrows_x);
+      const uint64_t pa = xa + static_cast<uint64_t>(row) * static_cast<uint64_t>(ldx) * 4u;
+      plo[q] = static_cast<uint32_t>(pa);
+      phi[q] = static_cast<uint32_t>(pa >> 32);
+    }
     // n per tile as well: the ~2P row-count conditions (64-bit masks) would
     // otherwise be hoisted and spilled to VGPR lanes (a v_readlane each)
     int n = n_arg;
     asm volatile("" : "+s"(n));
     const int k_bottom = MODE == 0 ? (P - n) / 2 : 0;
-    auto load = [&](int i, bool again = false) -> float {
-      int row = checked_row(__builtin_amdgcn_readlane(rl[i / 64], i % 64), nrows_x);
-      // the second pass recomputes the row base: kept from the first pass, the
-      // 128 64-bit bases would be held in (spilled) SGPRs across the network
-      if (again) asm volatile("" : "+s"(row));
-      const char* rp = uniform_ptr(reinterpret_cast<const char*>(X + static_cast<int64_t>(row) * ldx + base));
-      // default cache policy (not nt): step 2 re-reads these lines.  A/B at
-      // N=128, d=1e7: 2.06 ms (default) vs 2.14 (nt) per P=128 round; keeping
-      // an unsorted copy in registers instead (AGPR-backed): 2.63 ms
+    // row i's base (two readlanes into an SGPR pair, opaque: the second pass
+    // recomputes it -- kept from the first pass, the 128 64-bit bases would be
+    // held in spilled SGPRs across the network -- and the address stays an
+    // SGPR base + the lane's offset)
+    auto rowptr = [&](int i) -> uint64_t {
+      const uint32_t lo32 = __builtin_amdgcn_readlane(plo[i / 64], i % 64);
+      const uint32_t hi32 = __builtin_amdgcn_readlane(phi[i / 64], i % 64);
+      uint64_t rp = (static_cast<uint64_t>(hi32) << 32) | lo32;
+      asm volatile("" : "+s"(rp));
+      return rp;
+    };
+    // default cache policy (not nt): step 2 re-reads these lines.  A/B at
+    // N=128, d=1e7: 2.06 ms (default) vs 2.14 (nt) per P=128 round; keeping
+    // an unsorted copy in registers instead (AGPR-backed): 2.63 ms
+    auto ldp = [&](uint64_t rp) -> float {
       typedef const __attribute__((address_space(1))) float gfloat;
-      return *reinterpret_cast<gfloat*>(reinterpret_cast<uint64_t>(rp) + off);   // global_load, SGPR base
+      return *reinterpret_cast<gfloat*>(rp + off);   // global_load, SGPR base
+    };
+    // rows [first, first + count) in order, each base read two rows ahead of
+    // its load (a readlane-written SGPR read by the load right away costs a
+    // 5-cycle s_nop per row)
+    auto load_rows = [&](auto&& put, auto first_c, auto count_c) {
+      constexpr int first = decltype(first_c)::value, count = decltype(count_c)::value;
+      if constexpr (count > 0) {
+        uint64_t pa = rowptr(first);
+        uint64_t pb = count > 1 ? rowptr(first + 1) : 0;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < count; ++k) {
+          const uint64_t pc = k + 2 < count ? rowptr(first + k + 2) : 0;
+          __builtin_amdgcn_sched_barrier(0);
+          put(first + k, ldp(pa));
+          __builtin_amdgcn_sched_barrier(0);
+          pa = pb;
+          pb = pc;
+        }
+      }
     };
     constexpr int kFirstPad = P > 16 ? P - 16 : 0;   // rows below this are always real (n > P - 16)
     float v[P2];
-#pragma unroll
-    for (int i = 0; i < kFirstPad; ++i) {
-      v[i] = load(i);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    // lane i % 64 of block i / 64 holds rows[min(i, n - 1)] (clamped above);
+    // slots past n are padded
+    load_rows([&](int i, float x) { v[i] = x; }, std::integral_constant<int, 0>{}, std::integral_constant<int, P>{});
+    // after every load is in flight (a select right behind its load would
+    // wait for it there)
 #pragma unroll
     for (int i = kFirstPad; i < P; ++i) {
-      // lane i % 64 of block i / 64 holds rows[min(i, n - 1)] (clamped above)
-      const float x = load(i);
-      __builtin_amdgcn_sched_barrier(0);
       const float pad = (i - n < k_bottom) ? -__builtin_inff() : __builtin_inff();
-      v[i] = i < n ? x : pad;
+      v[i] = i < n ? v[i] : pad;
     }
-    // COPY: the unsorted column stays in registers for step 2 (no re-read)
-    float u[COPY ? P : 1];
-    if constexpr (COPY) {
+    const bool valid = t < rem;   // lanes past d contribute 0 to the distances
+    // the unsorted column for step 2: rows [0, KL) into LDS (zero past d),
+    // rows [KL, KU) stay in registers
+    if constexpr (KL > 0) {
 #pragma unroll
-      for (int i = 0; i < P; ++i) u[i] = v[i];
+      for (int i = 0; i < KL; ++i) dl[w][i][lane] = v[i];
+      if (rem < 256 && !valid) {   // ragged last tile only
+#pragma unroll
+        for (int i = 0; i < KL; ++i) dl[w][i][lane] = 0.f;
+      }
     }
+    constexpr int NU = KU > KL ? KU - KL : 0;
+    float u[NU > 0 ? NU : 1];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) u[i] = v[KL + i];
     // NaN detection over all slots (pads are +-inf, never NaN)
     float m = v[0];
 #pragma unroll
@@ -200,50 +256,50 @@ __global__ void __launch_bounds__(256, (COPY && P > 64) ? 2 : 3) select_dist_row
     }
     if (t < rem) out[base + t] = res;
     // step 2: squared distances of the listed rows over this wave's 64 coordinates
-    const bool valid = t < rem;   // lanes past d contribute 0
+    rsl[w][lane] = valid ? res : 0.f;
     // fresh copies of the row list: the first pass's 128 readlane results
     // (SGPRs) must not stay live across the network
 #pragma unroll
-    for (int q = 0; q < RW; ++q) asm volatile("" : "+v"(rl[q]));
+    for (int q = 0; q < RW; ++q) asm volatile("" : "+v"(plo[q]), "+v"(phi[q]));
+    // every re-read in flight at once, before the first chunk (the network's
+    // registers are free now): one cache latency per tile instead of one per
+    // chunk.  Rows past n are clamped copies of row n - 1 (sums never read).
+    constexpr int NR = P - (KU > KL ? KU : KL);
+    float xr[NR > 0 ? NR : 1];
+    load_rows([&](int i, float x) { xr[i - (P - NR)] = x; }, std::integral_constant<int, P - NR>{},
+              std::integral_constant<int, NR>{});
     const unsigned ti = lane & 31u, th = lane >> 5;
 #pragma unroll
     for (int c = 0; c < RW * 2; ++c) {
       if (32 * c >= n) break;   // wave-uniform
-      // all loads of the chunk in flight before the first use, unconditional
-      // (rows past n are clamped copies of row n - 1; their sums are never
-      // read): a per-row branch would serialise them on the cache latency
       constexpr int kChunkRows = 32;
-      float xs[kChunkRows];
 #pragma unroll
       for (int i = 0; i < kChunkRows; ++i) {
-        if (32 * c + i < P) {
-          if constexpr (COPY) {
-            xs[i] = u[32 * c + i];
-          } else {
-            xs[i] = load(32 * c + i, true);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < kChunkRows; ++i) {
-        if (32 * c + i < P) dl[w][i][lane] = res - xs[i];
+        const int r = 32 * c + i;
+        if (r < P && r >= KL) dl[w][i][lane] = r < P - NR ? u[r - KL] : xr[r - (P - NR)];
       }
       if (rem < 256 && !valid) {   // ragged last tile only: lanes past d add 0
 #pragma unroll
-        for (int i = 0; i < 32; ++i) dl[w][i][lane] = 0.f;
+        for (int i = 0; i < kChunkRows; ++i) {
+          const int r = 32 * c + i;
+          if (r < P && r >= KL) dl[w][i][lane] = 0.f;
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int rr = 32 * c + static_cast<int>(ti);
+      const int lrow = rr < KL ? rr : static_cast<int>(ti);
       float sh = 0.f;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const f32x4 q = *reinterpret_cast<const f32x4*>(&dl[w][ti][32 * th + 4 * u]);
-        sh = __builtin_fmaf(q[0], q[0], sh);
-        sh = __builtin_fmaf(q[1], q[1], sh);
-        sh = __builtin_fmaf(q[2], q[2], sh);
-        sh = __builtin_fmaf(q[3], q[3], sh);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&dl[w][lrow][32 * th + 4 * u]);
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&rsl[w][32 * th + 4 * u]);
+        const float q0 = a[0] - x[0], q1 = a[1] - x[1], q2 = a[2] - x[2], q3 = a[3] - x[3];
+        sh = __builtin_fmaf(q0, q0, sh);
+        sh = __builtin_fmaf(q1, q1, sh);
+        sh = __builtin_fmaf(q2, q2, sh);
+        sh = __builtin_fmaf(q3, q3, sh);
       }
       const float so = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(static_cast<int>((lane ^ 32u) * 4u),
                                                                               __builtin_bit_cast(int, sh)));
@@ -1088,12 +1144,32 @@ size_t bulyan_workspace_bytes(int n, int64_t d, int mode, int f) {
   return bulyan_body_bytes(n, d, mode, f) + sizeof(int64_t) * static_cast<size_t>(d);
 }
 
-// Rounds that keep the unsorted column in registers for the distance pass
-// (COPY) instead of re-reading it: same-box A/B at C3 (N = 128, d = 1e7, one
-// call): copies up to P = 64 / 96 / 112 -- trimmed mean 105.7 -> 103.4 /
-// 103.1 / 105.3 ms, median 92.2 -> 89.3 / 90.5 / 87.6 ms; P = 128 spills.
+// Where step 2 takes the columns from, per P (same-box per-round kernel times
+// at C3, profiles/r06_bulyan_rounds_ab.txt): up to P = 64 the whole column
+// stays in registers at three waves per SIMD; above, the first 44 rows go to
+// LDS (4 x 44 x 272 B + the aggregate and partial tiles = 50.9 KiB per
+// workgroup: three workgroups per CU, three waves per SIMD; 47 rows no longer
+// fit three) and the rest are re-read.  Register copies at two waves per SIMD
+// (P = 80 / 96 / 112) lost to the LDS form by 7-10 %.
+#ifndef SRA_BULYAN_COPY_MAX_MEDIAN
+#define SRA_BULYAN_COPY_MAX_MEDIAN 64
+#endif
+#ifndef SRA_BULYAN_COPY_MAX_TRIMMED
+#define SRA_BULYAN_COPY_MAX_TRIMMED 64
+#endif
 template <int P, int MODE>
-constexpr bool kCopyRows() { return MODE == 0 ? P <= 112 : P <= 96; }
+constexpr bool kCopyRows() {
+  return P <= 32 || (MODE == 0 ? P <= SRA_BULYAN_COPY_MAX_MEDIAN : P <= SRA_BULYAN_COPY_MAX_TRIMMED);
+}
+#ifndef SRA_BULYAN_LDS_ROWS
+#define SRA_BULYAN_LDS_ROWS 44
+#endif
+template <int P, int MODE>
+constexpr int kLdsRows() { return kCopyRows<P, MODE>() ? 0 : SRA_BULYAN_LDS_ROWS; }
+template <int P, int MODE>
+constexpr int kRegRows() { return kCopyRows<P, MODE>() ? P : kLdsRows<P, MODE>(); }
+template <int P, int MODE>
+constexpr int kRoundWaves() { return kCopyRows<P, MODE>() && P > 64 ? 2 : 3; }
 
 template <int MODE>
 static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int nrows_x, int n, int64_t d, int lo,
@@ -1103,7 +1179,8 @@ static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int 
   const int P = static_cast<int>(cdiv(n, 16) * 16);
 #define SRA_SR(PP)                                                                                             \
   case PP:                                                                                                     \
-    hipLaunchKernelGGL((select_dist_rows_kernel<PP, MODE, kCopyRows<PP, MODE>()>), dim3(blocks), dim3(256), 0, s, X, ldx, \
+    hipLaunchKernelGGL((select_dist_rows_kernel<PP, MODE, kLdsRows<PP, MODE>(), kRegRows<PP, MODE>(),             \
+                                                kRoundWaves<PP, MODE>()>), dim3(blocks), dim3(256), 0, s, X, ldx,      \
                        rows, nrows_x, n,                                                                       \
                        d, lo,                                                                                  \
                        hi, nan_all, out, bpart, static_cast<int>(blocks), static_cast<int>(tpb));                       \
