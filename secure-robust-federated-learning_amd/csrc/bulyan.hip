@@ -829,27 +829,53 @@ __global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(cons
   const int tl = rem <= 0 ? 0 : (t < rem ? t : static_cast<int>(rem - 1));
   const int64_t j = rem <= 0 ? d - 1 : base + tl;
   constexpr int RW = (P + 63) / 64;
-  int rl[RW];
-#pragma unroll
-  for (int q = 0; q < RW; ++q) {
-    const int li = 64 * q + t;
-    rl[q] = rows[li < theta ? li : theta - 1];
-  }
   const int64_t jb = j - tl;   // this wave's first coordinate (clamped)
   const unsigned off = static_cast<unsigned>(tl) * 4u;
+  // the selected rows' bases for this wave's coordinates, one 64-bit pointer
+  // per lane (lane l: rows[64 q + l], checked and clamped once); a row's base
+  // is then two readlanes, fetched two rows ahead of its load (see
+  // select_dist_rows_kernel)
+  uint32_t plo[RW], phi[RW];
+  auto row_bases = [&]() __attribute__((always_inline)) {
+    const uint64_t sa = reinterpret_cast<uint64_t>(S + jb);
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+      const int li = 64 * q + t;
+      const int row = checked_row(rows[li < theta ? li : theta - 1], nrows_s);
+      const uint64_t pa = sa + static_cast<uint64_t>(row) * static_cast<uint64_t>(lds_) * 4u;
+      plo[q] = static_cast<uint32_t>(pa);
+      phi[q] = static_cast<uint32_t>(pa >> 32);
+      asm volatile("" : "+v"(plo[q]), "+v"(phi[q]));
+    }
+  };
+  row_bases();
+  auto rowptr = [&](int i) -> uint64_t {
+    const uint32_t lo32 = __builtin_amdgcn_readlane(plo[i / 64], i % 64);
+    const uint32_t hi32 = __builtin_amdgcn_readlane(phi[i / 64], i % 64);
+    uint64_t rp = (static_cast<uint64_t>(hi32) << 32) | lo32;
+    asm volatile("" : "+s"(rp));
+    return rp;
+  };
   constexpr int kFirstPad = P > 16 ? P - 16 : 0;
   auto load_col = [&](float (&v)[P2], bool& nonfinite) __attribute__((always_inline)) {
+    uint64_t pa = rowptr(0), pb = P > 1 ? rowptr(1) : 0;
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-      const int row = checked_row(__builtin_amdgcn_readlane(rl[i / 64], i % 64), nrows_s);
-      const char* rp = uniform_ptr(reinterpret_cast<const char*>(S + static_cast<int64_t>(row) * lds_ + jb));
-      const float x = ld_lane(rp, off);
-      // one row address at a time in SGPRs (hoisting all of them spills)
+      const uint64_t pc = i + 2 < P ? rowptr(i + 2) : 0;
       __builtin_amdgcn_sched_barrier(0);
-      // rows below P - 16 always exist (theta > P - 16): no per-row predicate
+      v[i] = ld_lane(reinterpret_cast<const char*>(pa), off);
+      __builtin_amdgcn_sched_barrier(0);
+      pa = pb;
+      pb = pc;
+    }
+    // after every load is in flight: rows below P - 16 always exist
+    // (theta > P - 16), the rest are padded
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
       const bool real = i < kFirstPad || i < theta;
-      v[i] = real ? x : __builtin_inff();
-      nonfinite |= real && !__builtin_isfinite(x);
+      nonfinite |= real && !__builtin_isfinite(v[i]);
+      v[i] = real ? v[i] : __builtin_inff();
     }
   };
 
@@ -929,12 +955,7 @@ __global__ void __launch_bounds__(256, P <= 96 ? 4 : 2) bulyan_final_kernel(cons
       // even theta, two distinct middle values: np.argmin over the totals.
       // The row list is reloaded here, with every lane active, and kept opaque
       // (the first gather's row addresses are then not held live for reuse)
-#pragma unroll
-      for (int q = 0; q < RW; ++q) {
-        const int li = 64 * q + t;
-        rl[q] = rows[li < theta ? li : theta - 1];
-        asm volatile("" : "+v"(rl[q]));
-      }
+      row_bases();
       float o[P2];
       bool dummy = false;
       load_col(o, dummy);
