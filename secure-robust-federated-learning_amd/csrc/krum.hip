@@ -289,22 +289,45 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
     for (int u0 = 0; wave + nwaves * u0 < n; u0 += U) {
       // compaction of up to U rows
       if constexpr (STAGED) {
-        // N <= 128: each row is two 64-entry pieces; the U rows' LDS reads are
-        // independent, so they are issued together (no per-row latency chain)
+        // N <= 128: each row is two 64-entry pieces.  All 2U pieces' LDS
+        // reads are issued before any write (the compiler cannot tell the
+        // compaction buffer from the staged rows, so a write between them
+        // would serialise every piece on three LDS latencies); lanes with
+        // nothing to keep write the row's spare last slot (m <= n - 2 < GS - 1)
+        constexpr int NPC = 2 * U;
+        int js[NPC], ev[NPC];
+        bool rv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int i = wave + nwaves * (u0 + u);
-          const bool rv = i < n && alive[i < n ? i : 0];   // wave-uniform
+          rv[u] = (i < n) & (alive[i < n ? i : 0] != 0);   // wave-uniform
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int p = 64 * h2 + lane;
+            const int e = (i < n ? i : 0) * n + p;
+            ev[2 * u + h2] = p < n - 1 ? e : 0;
+            js[2 * u + h2] = Js[ev[2 * u + h2]];
+          }
+        }
+        bool okv[NPC];
+        float sv[NPC];
+#pragma unroll
+        for (int q = 0; q < NPC; ++q) {
+          const int p = 64 * (q & 1) + lane;
+          okv[q] = rv[q >> 1] & (p < n - 1) & (alive[js[q]] != 0);
+          sv[q] = Ss[ev[q]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
           int c = 0;
 #pragma unroll
-          for (int p0 = 0; p0 < 128; p0 += 64) {
-            const int p = p0 + lane;
-            const int e = (i < n ? i : 0) * n + p;
-            const bool ok = rv && p < n - 1 && alive[Js[p < n - 1 ? e : 0]];
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const bool ok = okv[2 * u + h2];
             const unsigned long long bal = __builtin_amdgcn_ballot_w64(ok);
             const int pre = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
                                                       __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
-            if (ok && c + pre < m) gw[u * GS + c + pre] = Ss[e];
+            const int dst = ok && c + pre < m ? c + pre : GS - 1;
+            gw[u * GS + dst] = sv[2 * u + h2];
             c += __builtin_popcountll(bal);
           }
         }
@@ -377,35 +400,37 @@ __global__ void __launch_bounds__(1024) krum_rounds_kernel(const float* __restri
     __syncthreads();
     if (wave == 0) {
       // np.argmin: first minimum; a NaN is the minimum (first NaN wins).
-      // key: (class 0 NaN / 1 number / 2 dead, value, index)
-      int bc = 2, bi = 0x7fffffff;
-      float bv = 0.f;
+      // One 64-bit key per row, (class 0 NaN / 1 number / 2 dead, value as
+      // order-preserving bits, index), so the wave minimum is two shuffles
+      // and one compare per step; -0 is taken as +0 (equal scores: the
+      // first index)
+      static_assert(kMaxClients <= 65536, "16-bit index field");
+      uint64_t best = ~0ull;
       for (int i = lane; i < n; i += 64) {
         const float v = score[i];
-        const int c = !alive[i] ? 2 : (v != v ? 0 : 1);
-        if (c < bc || (c == bc && c == 1 && v < bv)) {   // i ascends per lane: ties keep the first
-          bc = c;
-          bv = v;
-          bi = i;
+        const uint64_t cls = !alive[i] ? 2u : (v != v ? 0u : 1u);
+        uint32_t ob = 0;
+        if (cls == 1) {
+          const uint32_t b = __builtin_bit_cast(uint32_t, v + 0.0f);
+          ob = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
         }
+        const uint64_t k = (cls << 48) | (static_cast<uint64_t>(ob) << 16) | static_cast<uint64_t>(i);
+        best = k < best ? k : best;
       }
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) {
-        const int oc = __shfl_xor(bc, off);
-        const float ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
-        const bool better = oc < bc || (oc == bc && ((oc == 1 && ov < bv) || ((oc != 1 || ov == bv) && oi < bi)));
-        if (better) {
-          bc = oc;
-          bv = ov;
-          bi = oi;
-        }
+        const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(best >> 32), off));
+        const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(best), off));
+        const uint64_t o = (static_cast<uint64_t>(hi) << 32) | lo;
+        best = o < best ? o : best;
       }
+      const int bc = static_cast<int>(best >> 48);
+      const int bi = static_cast<int>(best & 0xffffu);
       if (lane == 0) {
-        const int best = bc < 2 ? bi : -1;
-        order[t] = best;
-        if (best >= 0) alive[best] = 0;
-        if (best < 0 && status) *status = 1;
+        const int pick = bc < 2 ? bi : -1;
+        order[t] = pick;
+        if (pick >= 0) alive[pick] = 0;
+        if (pick < 0 && status) *status = 1;
       }
     }
     if (t == 0 && scores0) {
