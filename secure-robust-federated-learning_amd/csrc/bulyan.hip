@@ -241,11 +241,27 @@ __global__ void __launch_bounds__(256, W) select_dist_rows_kernel(const float* _
       int lo_t = lo, hi_t = hi;
       asm volatile("" : "+s"(lo_t), "+s"(hi_t));
       float acc_s = 0.f;
+      // the trimmed mean's window, lo = int(0.1 n) <= A and hi = n - lo >= B
+      // for every n in (P - 16, P]: slots [A, B) are always summed, only the
+      // edges are conditional, and an edge slot outside the window adds -0
+      // (x + -0 == x for every x: the sum is bit-identical).  Any other
+      // window (the DBA lower median is one slot) takes the general loop.
+      constexpr int A = P / 10;
+      constexpr int B = (P > 16 ? P - 15 : 1) - (P > 16 ? P - 15 : 1) / 10;
+      if (lo_t <= A && hi_t >= B) {
 #pragma unroll
-      for (int p = OLO; p < OHI; ++p) {
-        if (p >= lo_t && p < hi_t) {
-          asm volatile("");
-          acc_s += v[p];
+        for (int p = OLO; p < A; ++p) acc_s += p >= lo_t ? v[p] : -0.0f;
+#pragma unroll
+        for (int p = A; p < B; ++p) acc_s += v[p];
+#pragma unroll
+        for (int p = B > A ? B : A; p < OHI; ++p) acc_s += p < hi_t ? v[p] : -0.0f;
+      } else {
+#pragma unroll
+        for (int p = OLO; p < OHI; ++p) {
+          if (p >= lo_t && p < hi_t) {
+            asm volatile("");
+            acc_s += v[p];
+          }
         }
       }
       res = acc_s / static_cast<float>(hi - lo);
