@@ -1246,7 +1246,9 @@ static int launch_select_dist(const float* X, int64_t ldx, const int* rows, int 
 static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows_s, int theta, int beta, int64_t d,
                         double* out, int* nf_count, int64_t* nf_list, hipStream_t s) {
   const int keep = bulyan_keep(theta, beta);
-  const int P = static_cast<int>(cdiv(theta, 16) * 16);
+  // theta rounded up to the round kernels' bucket width (the kernels assume
+  // only theta in (P - 16, P])
+  const int P = theta <= 16 ? 16 : static_cast<int>(cdiv(theta, kRoundBucket) * kRoundBucket);
   SRA_REQUIRE(theta >= 1 && theta <= kBigMaxClients, SRA_ERR_UNSUPPORTED,
               "bulyan per-coordinate stage supports theta <= %d (got %d)", kBigMaxClients, theta);
   SRA_HIP(hipMemsetAsync(nf_count, 0, sizeof(int), s));
@@ -1294,6 +1296,9 @@ static int launch_final(const float* S, int64_t lds_, const int* rows, int nrows
     return launch_status("bulyan_listed_kernel");
   switch (P) {
     SRA_FIN(16) SRA_FIN(32) SRA_FIN(48) SRA_FIN(64) SRA_FIN(80) SRA_FIN(96) SRA_FIN(112) SRA_FIN(128)
+#if SRA_BULYAN_BUCKET == 8
+    SRA_FIN(24) SRA_FIN(40) SRA_FIN(56) SRA_FIN(72) SRA_FIN(88) SRA_FIN(104) SRA_FIN(120)
+#endif
     default: break;
   }
 #undef SRA_FIN
